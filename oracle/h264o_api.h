@@ -1,0 +1,50 @@
+/*
+ * oracle/h264o_api.h -- TEST INFRASTRUCTURE ONLY. The CPU oracle's C API (loaded by tests/ via
+ * ctypes, by __graft_entry__.smoke() as the checker, and by bench.py's cpu_baseline leg). The
+ * product library (openh264-wasm_amd/, include/h264mi.h) never includes or links this.
+ *
+ * Parity status: the encoder restates OpenH264's algorithm at the wrapper's parameters but is
+ * "parity unpinned" against OpenH264 itself (no reference tests, fixtures or runnable build --
+ * see DESIGN.md §3); the decoder restates the normative H.264 decoding process.
+ */
+#ifndef H264O_API_H
+#define H264O_API_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct H264OEnc H264OEnc;
+typedef struct H264ODec H264ODec;
+
+/* encoder: mirrors init_encoder / force_key_frame / encode_frame_yuv_i420 (openh264_wrapper.cpp) */
+H264OEnc *h264o_enc_create(int w, int h, int bitrate);
+void h264o_enc_destroy(H264OEnc *e);
+void h264o_enc_force_idr(H264OEnc *e);
+int h264o_enc_encode(H264OEnc *e, const uint8_t *i420, uint8_t *out, int cap); /* bytes, 0 = fail */
+void h264o_enc_recon(const H264OEnc *e, uint8_t *i420_out);   /* deblocked recon, tight I420 */
+void h264o_enc_mbinfo(const H264OEnc *e, int32_t *out);       /* 8 x int32 per MB */
+int h264o_enc_last_qp(const H264OEnc *e);
+int h264o_rc_init_qp(int w, int h, int bitrate);
+int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr);
+size_t h264o_write_sps(int w, int h, uint8_t *out);
+size_t h264o_write_pps(uint8_t *out);
+
+/* decoder: mirrors init_decoder / decode_frame_yuv_i420 */
+H264ODec *h264o_dec_create(void);
+void h264o_dec_destroy(H264ODec *d);
+/* returns 1 when a picture was output into out_i420 (tight, cropped), 0 otherwise, <0 on error */
+int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out_i420, int *w, int *h);
+void h264o_dec_mbinfo(const H264ODec *d, int32_t *out);
+
+/* wrapper colour conversion: rgba_to_yuv (openh264_wrapper.cpp:22-40),
+ * yuv_to_rgba_optimized (:150-195) */
+void h264o_rgba_to_i420(const uint8_t *rgba, int w, int h, uint8_t *i420_out);
+void h264o_i420_to_rgba(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int ys, int uvs,
+                        uint8_t *rgba_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
