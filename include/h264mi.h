@@ -1,0 +1,80 @@
+/*
+ * include/h264mi.h -- C-ABI of libh264mi (openh264-wasm_amd/lib/libh264mi.so), the MI355X-native
+ * H.264 encode/decode core that replaces openh264_wrapper.cpp + OpenH264 on the reference's hot
+ * path. Plain C types only; no HIP or torch types in any signature.
+ *
+ * Part 1 -- drop-in wrapper surface. Each declaration below replaces the reference function of the
+ * same name (file:line in /root/reference/openh264_wrapper.cpp) with identical argument meaning,
+ * ownership and error behaviour, and is what the reference's JS glue binds through
+ * Module.cwrap(...) (scripts/encoder_worker.js:27-29, scripts/decoder_worker.js:346-349):
+ *   - init_* return 0 on success, -1 on failure;
+ *   - the void functions report failure / "no picture" through zeroed out-params;
+ *   - the encoded buffer is library-owned and valid until the next encode_* call;
+ *   - decoder indices 0..31 (MAX_DECODERS); invalid index = silent no-op.
+ */
+#ifndef H264MI_H
+#define H264MI_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* openh264_wrapper.cpp:198-228 */
+int init_encoder(int width, int height, int bitrate);
+/* openh264_wrapper.cpp:230-236 */
+void force_key_frame(void);
+/* openh264_wrapper.cpp:240-251 */
+void deinit_decoder(int decoder_index);
+/* openh264_wrapper.cpp:253-280 */
+int init_decoder(int decoder_index);
+/* openh264_wrapper.cpp:315-356 (RGBA8 input, converted with rgba_to_yuv :22-40 on the GPU) */
+void encode_frame(unsigned char *rgba_data, int width, int height, unsigned char **out_data, int *out_size);
+/* openh264_wrapper.cpp:358-389 (tight I420 input) */
+void encode_frame_yuv_i420(unsigned char *yuv_i420_data, int width, int height, unsigned char **out_data, int *out_size);
+/* openh264_wrapper.cpp:391-422 (RGBA8 output via yuv_to_rgba_optimized :150-195 on the GPU) */
+void decode_frame_optimized(int decoder_index, unsigned char *encoded_data, int size, unsigned char *out_rgba_buffer,
+                            int *out_width, int *out_height);
+/* openh264_wrapper.cpp:424-464 (tight I420 output) */
+void decode_frame_yuv_i420(int decoder_index, unsigned char *encoded_data, int size, unsigned char *out_yuv_buffer,
+                           int *out_width, int *out_height);
+/* openh264_wrapper.cpp:466-471 */
+void free_buffer(void *ptr);
+
+/*
+ * Part 2 -- device-resident batch API (no reference counterpart: it is the MI355X-native way to
+ * drive the same path for many independent streams whose frames/NAL units already live in HBM).
+ * All "d_" pointers are device pointers; hip_stream is a hipStream_t (or NULL for an internal one).
+ */
+typedef struct h264mi_encoder h264mi_encoder;
+h264mi_encoder *h264mi_enc_create(int width, int height, int bitrate, int nstreams, void *hip_stream);
+void h264mi_enc_destroy(h264mi_encoder *e);
+int h264mi_enc_force_idr(h264mi_encoder *e, int stream);            /* stream < 0: all */
+int h264mi_enc_encode(h264mi_encoder *e, const void *d_frames);     /* async; nstreams tight I420 frames back to back */
+int h264mi_enc_sync(h264mi_encoder *e);
+int h264mi_enc_nal_bytes(h264mi_encoder *e, int *out_bytes);        /* sync; -2 if a kernel reported an error */
+const void *h264mi_enc_nal_ptr(h264mi_encoder *e, int stream);     /* Annex-B bytes of the last frame (device) */
+const void *h264mi_enc_recon_ptr(h264mi_encoder *e, int stream);   /* deblocked reconstruction, coded size (device) */
+const void *h264mi_enc_input_buffer(h264mi_encoder *e);            /* internal device input area (nstreams frames) */
+size_t h264mi_enc_frame_bytes(h264mi_encoder *e);
+int h264mi_enc_last_qp(h264mi_encoder *e, int stream);
+int h264mi_enc_mbinfo(h264mi_encoder *e, int stream, void *host_out); /* 128 B per MB (h264mi_types.h MbInfo) */
+void *h264mi_enc_stream(h264mi_encoder *e);
+
+typedef struct h264mi_decoder h264mi_decoder;
+h264mi_decoder *h264mi_dec_create(int width, int height, int nstreams, void *hip_stream);
+void h264mi_dec_destroy(h264mi_decoder *d);
+/* async; d_nal[s] / nal_bytes[s] (host array) per stream; a stream with nal_bytes 0 is skipped */
+int h264mi_dec_decode(h264mi_decoder *d, const void *const *d_nal, const int *nal_bytes);
+int h264mi_dec_sync(h264mi_decoder *d);
+int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
+const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */
+int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
+void *h264mi_dec_stream(h264mi_decoder *d);
+
+/* library self-description */
+const char *h264mi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

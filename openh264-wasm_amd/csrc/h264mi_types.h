@@ -1,0 +1,105 @@
+// h264mi_types.h -- HBM data layout shared by the host runtime and the gfx950 kernels.
+//
+// One "stream" = one independent encoder (or decoder) instance. Every per-stream buffer lives in
+// HBM for the lifetime of the instance; a batch of S streams of the same geometry is driven by one
+// launch per pipeline stage.
+#pragma once
+#include <stdint.h>
+
+#define H264MI_MAX_STREAMS 256
+#define H264MI_MB_SLOT_DWORDS 640      // per-MB CAVLC scratch (20480 bits; worst case < 17.6 kbit)
+#define H264MI_GRANULES_PER_MB 16      // row-to-row hand-off record (8-byte {tag,payload} granules)
+#define H264MI_DBK_GRANULES_PER_MB 24  // deblocking hand-off (luma rows 12..15, chroma rows 6..7)
+
+enum { MI_I4 = 0, MI_I16 = 1, MI_P16x16 = 2, MI_PSKIP = 3, MI_P16x8 = 4, MI_P8x16 = 5, MI_P8x8 = 6, MI_IPCM = 7 };
+
+// Per-macroblock side information (128 B). Written by the MB wavefront kernel (encoder) or the
+// parse kernel (decoder); read by CAVLC, reconstruction and deblocking.
+struct MbInfo {
+    uint8_t type, qp, cbp, i16mode;
+    uint8_t cmode, qpc, pad0, pad1;
+    int8_t i4mode[16];   // raster 4x4 order; 2 (DC) for non-I4 macroblocks
+    int8_t ref[4];       // per 8x8, -1 intra
+    uint8_t nnz[24];     // TotalCoeff: luma raster 0..15, Cb 16..19, Cr 20..23
+    int16_t mvd[2];      // encoder P16x16 mvd
+    uint8_t sub[4];      // decoder P8x8 sub_mb_type
+    int16_t mv[16][2];   // raster 4x4, quarter-pel
+    int32_t pad2;
+};
+static_assert(sizeof(MbInfo) == 128, "MbInfo layout");
+
+// Quantised levels (scan order). Blocks whose TotalCoeff is 0 are not written and must not be read.
+struct MbCoef {
+    int16_t luma[16][16];   // raster luma block, scan index (I16: index 0 unused)
+    int16_t cac[2][4][16];  // chroma AC, scan index 0 unused
+    int16_t lumadc[16];     // I16 DC, scan order
+    int16_t cdc[2][4];      // chroma DC
+    int16_t pad[8];
+};
+static_assert(sizeof(MbCoef) == 832, "MbCoef layout");
+
+// Per-stream encoder state (device resident; read/updated by the frame-begin and pack kernels).
+struct EncState {
+    int32_t qp;            // QP for the next frame (rate control output)
+    int32_t cur_qp;        // QP of the frame being coded
+    int32_t cur_idr;       // 1 if the frame being coded is IDR
+    int32_t force_idr;     // host request (force_key_frame)
+    int32_t first;         // no frame coded yet
+    int32_t frame_num, idr_pic_id, poc;
+    uint32_t epoch;        // hand-off tag, +1 per coded frame (never 0)
+    int32_t bitrate;
+    int32_t nal_bytes;     // bytes of the last coded frame (all NAL units, start codes included)
+    int32_t err;           // nonzero: a kernel detected an error / timeout
+    int64_t last_bits;
+    int32_t sps_bytes, pps_bytes;
+    uint8_t sps[64], pps[32];
+};
+
+// Per-stream encoder buffers for one frame step.
+struct EncDesc {
+    const uint8_t *src;     // tight I420 input (w x h), planes contiguous
+    uint8_t *rec[3];        // unfiltered reconstruction (coded size)
+    const uint8_t *ref[3];  // deblocked previous frame (coded size)
+    uint8_t *dbk[3];        // deblocked output of this frame (coded size) -> next ref
+    MbInfo *info;
+    MbCoef *coef;
+    uint64_t *gran;         // MB-row hand-off granules
+    uint64_t *dgran;        // deblocking hand-off granules
+    uint32_t *mbbits;       // per-MB CAVLC bits, H264MI_MB_SLOT_DWORDS each
+    uint32_t *mblen;        // per-MB bit count (0 = P_Skip)
+    uint32_t *rbsp;         // slice RBSP scratch (dwords)
+    uint8_t *nal;           // Annex-B output of this frame
+    EncState *st;
+    int32_t nal_cap;
+    int32_t rbsp_cap;       // dwords
+};
+
+// Per-stream decoder state + buffers.
+struct DecState {
+    int32_t have_sps, have_pps;
+    int32_t mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4];
+    int32_t num_ref_default, pic_init_qp, cqp_off, dbk_ctrl, constrained_intra, redundant, bottom_field_poc, weighted;
+    int32_t has_ref;
+    int32_t got_pic;       // 1 if the last call produced a picture
+    int32_t slice_qp, dbk_idc;
+    int32_t err;
+    uint32_t epoch;
+    int32_t out_w, out_h;
+};
+
+struct DecDesc {
+    const uint8_t *nal;     // Annex-B input
+    int32_t nal_bytes;
+    int32_t pad;
+    uint8_t *rbsp;          // scratch (EP removed)
+    uint8_t *cur[3];        // reconstruction (coded size)
+    const uint8_t *ref[3];
+    uint8_t *dbk[3];        // deblocked output -> display + next ref
+    MbInfo *info;
+    MbCoef *coef;
+    uint64_t *gran;
+    uint64_t *dgran;
+    DecState *st;
+    int32_t rbsp_cap;
+    int32_t cw, ch;         // allocated coded size
+};

@@ -409,8 +409,8 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
         return;
     }
     /* 2. integer ME: candidates, then iterated small diamond */
-    int xmin = -16 * mbx - 16, xmax = 16 * (e->mbw - 1 - mbx) + 16;
-    int ymin = -16 * mby - 16, ymax = 16 * (e->mbh - 1 - mby) + 16;
+    /* integer search range: +-16 pel around (0,0) */
+    const int xmin = -16, xmax = 16, ymin = -16, ymax = 16;
     int cand[2][2] = {{(mvp[0] + 2) >> 2, (mvp[1] + 2) >> 2}, {0, 0}};
     int bx = 0, by = 0, bc = -1;
     for (int i = 0; i < 2; i++) {
