@@ -71,6 +71,10 @@ const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked 
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
 void *h264mi_dec_stream(h264mi_decoder *d);
 
+/* edge colour conversions on the GPU, host buffers (openh264_wrapper.cpp:22-40 and :150-195) */
+int h264mi_rgba_to_i420_host(const unsigned char *rgba, int width, int height, unsigned char *out_i420);
+int h264mi_i420_to_rgba_host(const unsigned char *i420, int width, int height, unsigned char *out_rgba);
+
 /* library self-description */
 const char *h264mi_version(void);
 

@@ -84,22 +84,17 @@ struct DecState {
     int32_t slice_qp, dbk_idc;
     int32_t err;
     uint32_t epoch;
+    int32_t parity;        // pic[parity] = last output picture = reference for the next P slice
     int32_t out_w, out_h;
 };
 
 struct DecDesc {
-    const uint8_t *nal;     // Annex-B input
-    int32_t nal_bytes;
-    int32_t pad;
-    uint8_t *rbsp;          // scratch (EP removed)
-    uint8_t *cur[3];        // reconstruction (coded size)
-    const uint8_t *ref[3];
-    uint8_t *dbk[3];        // deblocked output -> display + next ref
+    uint8_t *cur[3];        // unfiltered reconstruction (coded size)
+    uint8_t *pic[2][3];     // deblocked pictures (ping-pong by DecState::parity)
     MbInfo *info;
     MbCoef *coef;
     uint64_t *gran;
     uint64_t *dgran;
     DecState *st;
-    int32_t rbsp_cap;
     int32_t cw, ch;         // allocated coded size
 };

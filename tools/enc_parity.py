@@ -6,7 +6,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
 from h264mi.synth import SyntheticStream
 
-def main(w, h, br, nf, force_every=0):
+def main(w, h, br, nf, force_every=0, rgba=0):
     O = ctypes.CDLL(os.path.join(ROOT, 'oracle/build/libh264_oracle.so'))
     O.h264o_enc_create.restype = ctypes.c_void_p
     G = ctypes.CDLL(os.path.join(ROOT, 'openh264-wasm_amd/lib/libh264mi.so'))
@@ -19,13 +19,20 @@ def main(w, h, br, nf, force_every=0):
     ok = True
     for t in range(nf):
         f = np.ascontiguousarray(S.frame(t))
+        if rgba:  # RGBA input path (encode_frame): RGBA from a seeded generator, converted by both sides
+            rng = np.random.default_rng(t)
+            rgb = np.repeat(np.repeat(rng.integers(0, 256, (h // 2, w // 2, 4), dtype=np.uint8), 2, 0), 2, 1)
+            rgb = np.ascontiguousarray(((rgb.astype(np.uint16) + np.roll(rgb, 1, 1)) // 2).astype(np.uint8))
+            f = np.zeros(w * h * 3 // 2, np.uint8)
+            O.h264o_rgba_to_i420(rgb.ctypes.data_as(ctypes.c_void_p), w, h, f.ctypes.data_as(ctypes.c_void_p))
         if force_every and t % force_every == 0 and t > 0:
             O.h264o_enc_force_idr(e); G.force_key_frame()
         n = O.h264o_enc_encode(e, f.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(out.size))
         ref = out[:n].tobytes()
         p = ctypes.POINTER(ctypes.c_ubyte)(); sz = ctypes.c_int(0)
         t0 = time.time()
-        G.encode_frame_yuv_i420(f.ctypes.data_as(ctypes.c_void_p), w, h, ctypes.byref(p), ctypes.byref(sz))
+        if rgba: G.encode_frame(rgb.ctypes.data_as(ctypes.c_void_p), w, h, ctypes.byref(p), ctypes.byref(sz))
+        else: G.encode_frame_yuv_i420(f.ctypes.data_as(ctypes.c_void_p), w, h, ctypes.byref(p), ctypes.byref(sz))
         dt = time.time() - t0
         got = ctypes.string_at(p, sz.value) if sz.value > 0 else b''
         same = got == ref
