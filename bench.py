@@ -1,0 +1,215 @@
+#!/usr/bin/env python
+"""bench.py -- BASELINE.json metric "1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264".
+
+One step = one frame of every stream this rank owns: GPU encode (libh264mi batch encoder, IPPP,
+intra period 0, wrapper parameters, 1 Mbps) immediately followed by the GPU decode of the NAL units
+it produced; at N > 1 the step also gathers every rank's NAL units to rank 0 over RCCL (config 5:
+32 streams = 4 per GPU x 8 GPUs). Inputs are synthetic 1080p I420 clips resident in HBM before the
+timed region. value = frames encoded+decoded by all ranks / max-over-ranks wall time.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=60)
+    ap.add_argument('--warmup', type=int, default=4)
+    ap.add_argument('--streams', type=int, default=4, help='streams per GPU (config 5: 32 streams / 8 GPUs)')
+    ap.add_argument('--width', type=int, default=1920)
+    ap.add_argument('--height', type=int, default=1080)
+    ap.add_argument('--bitrate', type=int, default=1000000)
+    ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-frames', type=int, default=16)
+    ap.add_argument('--cpu-procs', type=int, default=16)
+    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'pmc_enc_mb.json'))
+    return ap.parse_args()
+
+
+def cpu_baseline(a):
+    procs = min(a.cpu_procs, os.cpu_count() or 1)
+    cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
+           '--bitrate', str(a.bitrate), '--frames', str(a.cpu_frames), '--procs', str(procs)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        line = [l for l in r.stdout.splitlines() if l.startswith('{')][-1]
+        d = json.loads(line)
+        return {k: d[k] for k in ('value', 'unit', 'cores', 'kind', 'sample')}
+    except Exception as e:  # reported, never silently replaced
+        return {'value': None, 'unit': 'frames/s', 'cores': procs, 'kind': 'port', 'sample': f'failed: {e!r}'}
+
+
+def gather_nals_to_rank0(dist, torch, nal_buf, sizes_dev, S, slot, rank, world):
+    """RCCL gatherv of this step's NAL units to rank 0: all_gather of the per-stream byte counts,
+    then exact-size point-to-point sends (batch_isend_irecv) of each stream's slot prefix.
+    Returns (on rank 0) a list of world*S byte counts; the payloads land in the receive buffer."""
+    sizes_all = torch.empty(world * S, dtype=torch.int32, device=sizes_dev.device)
+    dist.all_gather_into_tensor(sizes_all, sizes_dev)
+    sz = sizes_all.cpu().tolist()
+    ops = []
+    if rank == 0:
+        rx = gather_nals_to_rank0.rx
+        for r in range(1, world):
+            for s in range(S):
+                n = sz[r * S + s]
+                if n > 0:
+                    ops.append(dist.P2POp(dist.irecv, rx[(r * S + s) * slot:(r * S + s) * slot + n], r))
+    else:
+        for s in range(S):
+            n = sz[rank * S + s]
+            if n > 0:
+                ops.append(dist.P2POp(dist.isend, nal_buf[s * slot:s * slot + n], 0))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return sz
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if a.gpus != world and world > 1:
+        print(f'warning: --gpus {a.gpus} but WORLD_SIZE {world}', file=sys.stderr)
+    # CPU baseline first, in child processes, before this process touches the GPU (rank 0, N = 1)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a)
+
+    import numpy as np
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    W, H, S = a.width, a.height, a.streams
+    F = W * H * 3 // 2
+    # ---- synthetic clips, resident in HBM: clip[t] = S frames back to back
+    clip = torch.empty((a.clip, S * F), dtype=torch.uint8, device=dev)
+    for i in range(S):
+        g = SyntheticStream(rank * S + i, W, H)
+        host = np.stack([g.frame(t) for t in range(a.clip)])
+        clip[:, i * F:(i + 1) * F].copy_(torch.from_numpy(host))
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=stream)
+    dec = h264mi.BatchDecoder(W, H, S, stream=stream)
+    size_ptrs = enc.nal_size_ptrs()
+    slot = 1 << 21
+    nal_buf = sizes_dev = None
+    if world > 1:
+        nal_buf = torch.empty(S * slot, dtype=torch.uint8, device=dev)
+        sizes_dev = torch.empty(S, dtype=torch.int32, device=dev)
+        if rank == 0:
+            gather_nals_to_rank0.rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev)
+
+    step_no = [0]
+
+    def step():
+        t = step_no[0]
+        enc.encode(clip[t % a.clip])
+        dec.decode_dev(enc.nal_ptrs(), size_ptrs)
+        if world > 1:
+            enc.copy_nals(nal_buf, slot, sizes_dev)
+            gather_nals_to_rank0(dist, torch, nal_buf, sizes_dev, S, slot, rank, world)
+        step_no[0] += 1
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    # ---- parity self-check before timing: decoder output == encoder reconstruction, every stream
+    rc, got = dec.status()
+    parity_ok = rc == 0 and all(got)
+    import ctypes
+    for s in range(S):
+        cw, ch = dec.cw, dec.ch
+        a_ = torch.empty(cw * ch * 3 // 2, dtype=torch.uint8, device=dev)
+        b_ = torch.empty_like(a_)
+        hip = h264mi._hiprt()
+        hip.hipMemcpy(ctypes.c_void_p(a_.data_ptr()), ctypes.c_void_p(enc.recon_ptr(s)), ctypes.c_size_t(a_.numel()), 3)
+        hip.hipMemcpy(ctypes.c_void_p(b_.data_ptr()), ctypes.c_void_p(dec._L.h264mi_dec_picture_ptr(dec._d, s)),
+                      ctypes.c_size_t(b_.numel()), 3)
+        parity_ok = parity_ok and bool(torch.equal(a_, b_))
+    # ---- timed region
+    enc.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kms, nl = enc.kernel_time()
+    enc.set_timing(False)
+    sizes = enc.nal_sizes()
+    if dist:
+        tt = torch.tensor([elapsed, kms / max(nl, 1)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kavg = float(tt[0]), float(tt[1])
+        ok = torch.tensor([1 if parity_ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity_ok = bool(ok.item())
+    else:
+        kavg = kms / max(nl, 1)
+    frames = S * world * a.steps
+    value = frames / elapsed
+    # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
+    # (read source F + read reference F + write reconstruction F) for a P frame
+    alg_bytes = S * 3 * F
+    achieved = alg_bytes / (kavg / 1e3) / 1e9
+    traffic = None
+    if os.path.exists(a.traffic):
+        try:
+            tj = json.load(open(a.traffic))
+            if tj.get('width') == W and tj.get('height') == H and tj.get('streams') == S:
+                traffic = tj.get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    if rank == 0:
+        out = {
+            'metric': '1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264',
+            'value': value, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+            'config': {'workload': f'{W}x{H} IPPP encode+decode (intra period 0), {S} streams per GPU, '
+                                   f'{a.bitrate} bps, wrapper encoder params; NAL gather to rank 0 at N>1',
+                       'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate,
+                       'parallelism': f'streams x{world} (weak)'},
+            'roofline': {'bound': 'hbm', 'kernel': 'enc_mb_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBPS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
+                         'alg_bytes_per_launch': alg_bytes, 'avg_launch_ms': kavg},
+            'cpu_baseline': cpu,
+            'parity_selfcheck': 'decoder output == encoder reconstruction for every stream: ' + ('pass' if parity_ok else 'FAIL'),
+            'last_nal_bytes': sizes,
+        }
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

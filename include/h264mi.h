@@ -59,12 +59,18 @@ size_t h264mi_enc_frame_bytes(h264mi_encoder *e);
 int h264mi_enc_last_qp(h264mi_encoder *e, int stream);
 int h264mi_enc_mbinfo(h264mi_encoder *e, int stream, void *host_out); /* 128 B per MB (h264mi_types.h MbInfo) */
 void *h264mi_enc_stream(h264mi_encoder *e);
+const int *h264mi_enc_nal_size_dev(h264mi_encoder *e, int stream); /* device address of the NAL byte count */
+int h264mi_enc_copy_nals(h264mi_encoder *e, void *d_dst, int slot_bytes, int *d_sizes); /* async: s -> d_dst+s*slot */
+int h264mi_enc_set_timing(h264mi_encoder *e, int enable);          /* HIP events around the MB kernel */
+int h264mi_enc_kernel_time(h264mi_encoder *e, double *ms_total, int *launches);
 
 typedef struct h264mi_decoder h264mi_decoder;
 h264mi_decoder *h264mi_dec_create(int width, int height, int nstreams, void *hip_stream);
 void h264mi_dec_destroy(h264mi_decoder *d);
 /* async; d_nal[s] / nal_bytes[s] (host array) per stream; a stream with nal_bytes 0 is skipped */
 int h264mi_dec_decode(h264mi_decoder *d, const void *const *d_nal, const int *nal_bytes);
+/* async; NAL sizes read from device memory (e.g. h264mi_enc_nal_size_dev): no host round trip */
+int h264mi_dec_decode_dev(h264mi_decoder *d, const void *const *d_nal, const int *const *d_sizes);
 int h264mi_dec_sync(h264mi_decoder *d);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */

@@ -1,0 +1,329 @@
+"""h264mi -- Python host bindings of libh264mi (MI355X-native H.264 encode/decode core).
+
+Layering:
+  * ``lib/libh264mi.so`` -- HIP kernels for gfx950 + runtime + the C-ABI declared in
+    ``include/h264mi.h``.
+  * ``Module`` (this file) -- mirrors the Emscripten ``Module`` object the reference's workers use
+    (``cwrap``/``_malloc``/``_free``/``getValue``/``HEAPU8``; scripts/encoder_worker.js:27-29,
+    decoder_worker.js:346-349) so call sequences read exactly like the reference's glue.
+  * ``BatchEncoder`` / ``BatchDecoder`` -- the device-resident multi-stream API (frames and NAL
+    units already in HBM) used by bench.py and the multi-GPU path.
+
+There is no CPU fallback: importing this module on a machine without the built library raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), 'lib', 'libh264mi.so')
+
+_lib = None
+
+
+def lib():
+    """Load libh264mi.so (fails loudly when it is missing -- there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'libh264mi.so not built ({LIB_PATH}); run openh264-wasm_amd/build.py')
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i, cp = ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p
+        sig = {
+            'init_encoder': (i, [i, i, i]),
+            'force_key_frame': (None, []),
+            'init_decoder': (i, [i]),
+            'deinit_decoder': (None, [i]),
+            'encode_frame': (None, [vp, i, i, vp, vp]),
+            'encode_frame_yuv_i420': (None, [vp, i, i, vp, vp]),
+            'decode_frame_optimized': (None, [i, vp, i, vp, vp, vp]),
+            'decode_frame_yuv_i420': (None, [i, vp, i, vp, vp, vp]),
+            'free_buffer': (None, [vp]),
+            'h264mi_enc_create': (vp, [i, i, i, i, vp]),
+            'h264mi_enc_destroy': (None, [vp]),
+            'h264mi_enc_force_idr': (i, [vp, i]),
+            'h264mi_enc_encode': (i, [vp, vp]),
+            'h264mi_enc_sync': (i, [vp]),
+            'h264mi_enc_nal_bytes': (i, [vp, vp]),
+            'h264mi_enc_nal_ptr': (vp, [vp, i]),
+            'h264mi_enc_recon_ptr': (vp, [vp, i]),
+            'h264mi_enc_input_buffer': (vp, [vp]),
+            'h264mi_enc_frame_bytes': (ctypes.c_size_t, [vp]),
+            'h264mi_enc_last_qp': (i, [vp, i]),
+            'h264mi_enc_mbinfo': (i, [vp, i, vp]),
+            'h264mi_enc_stream': (vp, [vp]),
+            'h264mi_enc_nal_size_dev': (vp, [vp, i]),
+            'h264mi_enc_copy_nals': (i, [vp, vp, i, vp]),
+            'h264mi_enc_set_timing': (i, [vp, i]),
+            'h264mi_enc_kernel_time': (i, [vp, vp, vp]),
+            'h264mi_dec_decode_dev': (i, [vp, vp, vp]),
+            'h264mi_dec_create': (vp, [i, i, i, vp]),
+            'h264mi_dec_destroy': (None, [vp]),
+            'h264mi_dec_decode': (i, [vp, vp, vp]),
+            'h264mi_dec_sync': (i, [vp]),
+            'h264mi_dec_status': (i, [vp, vp]),
+            'h264mi_dec_picture_ptr': (vp, [vp, i]),
+            'h264mi_dec_coded_size': (i, [vp, vp, vp]),
+            'h264mi_dec_stream': (vp, [vp]),
+            'h264mi_rgba_to_i420_host': (i, [vp, i, i, vp]),
+            'h264mi_i420_to_rgba_host': (i, [vp, i, i, vp]),
+            'h264mi_version': (cp, []),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+EXPORTED = ('init_encoder', 'force_key_frame', 'init_decoder', 'deinit_decoder', 'encode_frame',
+            'encode_frame_yuv_i420', 'decode_frame_optimized', 'decode_frame_yuv_i420', 'free_buffer')
+
+
+class Module:
+    """Emscripten-``Module``-shaped facade over the C-ABI (the reference's JS glue surface).
+
+    ``HEAPU8`` is a bytearray arena; ``_malloc`` returns offsets into it; ``cwrap`` returns callables
+    that translate arena offsets to native pointers (and native output pointers back into arena
+    offsets, e.g. the encoded buffer of encode_frame*), exactly as the workers expect
+    (encoder_worker.js:163-187 reads the encoded buffer via getValue + HEAPU8.subarray).
+    """
+
+    def __init__(self, heap_bytes=64 << 20):
+        self._L = lib()
+        self.HEAPU8 = bytearray(heap_bytes)
+        self._heap = (ctypes.c_ubyte * heap_bytes).from_buffer(self.HEAPU8)
+        self._base = ctypes.addressof(self._heap)
+        self._brk = 16
+        self._freelist = {}  # offset -> size (first-fit)
+        self._sizes = {}
+        self._out_off, self._out_cap = 0, 0
+
+    # -- heap management (Module._malloc / Module._free)
+    def _malloc(self, n):
+        n = (max(1, int(n)) + 15) & ~15
+        for off, sz in sorted(self._freelist.items()):
+            if sz >= n:
+                del self._freelist[off]
+                if sz > n:
+                    self._freelist[off + n] = sz - n
+                self._sizes[off] = n
+                return off
+        off = self._brk
+        if off + n > len(self.HEAPU8):
+            raise MemoryError('h264mi Module heap exhausted')
+        self._brk += n
+        self._sizes[off] = n
+        return off
+
+    def _free(self, off):
+        n = self._sizes.pop(off, None)
+        if n:
+            self._freelist[off] = n
+
+    def getValue(self, ptr, typ='i32'):
+        assert typ == 'i32'
+        return int.from_bytes(self.HEAPU8[ptr:ptr + 4], 'little', signed=True)
+
+    def setValue(self, ptr, value, typ='i32'):
+        assert typ == 'i32'
+        self.HEAPU8[ptr:ptr + 4] = int(value).to_bytes(4, 'little', signed=True)
+
+    def _p(self, off):
+        return ctypes.c_void_p(self._base + off)
+
+    def cwrap(self, name, ret, args):
+        if name not in EXPORTED:
+            raise KeyError(f'{name} is not exported by libh264mi')
+        f = getattr(self._L, name)
+        if name in ('encode_frame', 'encode_frame_yuv_i420'):
+            def enc(src, w, h, out_pp, out_size_p, _f=f):
+                native = ctypes.POINTER(ctypes.c_ubyte)()
+                size = ctypes.c_int(0)
+                _f(self._p(src), w, h, ctypes.byref(native), ctypes.byref(size))
+                if size.value <= 0:
+                    self.setValue(out_pp, 0)
+                    self.setValue(out_size_p, 0)
+                    return None
+                if size.value > self._out_cap:  # library-owned output mirrored into the heap
+                    if self._out_cap:
+                        self._free(self._out_off)
+                    self._out_off, self._out_cap = self._malloc(size.value), size.value
+                ctypes.memmove(self._base + self._out_off, native, size.value)
+                self.setValue(out_pp, self._out_off)
+                self.setValue(out_size_p, size.value)
+                return None
+            return enc
+        if name in ('decode_frame_optimized', 'decode_frame_yuv_i420'):
+            def dec(idx, nal, size, out, w_p, h_p, _f=f):
+                _f(idx, self._p(nal), size, self._p(out), self._p(w_p), self._p(h_p))
+                return None
+            return dec
+        if name == 'free_buffer':
+            return lambda ptr: None  # the reference glue never frees the library-owned buffer
+        return lambda *a: f(*a)
+
+    def on_runtime_initialized(self, cb):
+        cb()
+
+
+class BatchEncoder:
+    """S independent encoder streams of one geometry, frames and NAL units resident in HBM."""
+
+    def __init__(self, width, height, bitrate, nstreams, stream=None):
+        import torch
+        self.w, self.h, self.S = width, height, nstreams
+        self.frame_bytes = width * height * 3 // 2
+        self._L = lib()
+        hs = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._e = self._L.h264mi_enc_create(width, height, bitrate, nstreams, ctypes.c_void_p(hs))
+        if not self._e:
+            raise RuntimeError('h264mi_enc_create failed')
+
+    def encode(self, frames):
+        """frames: uint8 CUDA tensor holding S tight I420 frames back to back (async)."""
+        assert frames.is_cuda and frames.numel() >= self.S * self.frame_bytes
+        if self._L.h264mi_enc_encode(self._e, ctypes.c_void_p(frames.data_ptr())) != 0:
+            raise RuntimeError('h264mi_enc_encode failed')
+
+    def force_idr(self, stream=-1):
+        self._L.h264mi_enc_force_idr(self._e, stream)
+
+    def nal_sizes(self):
+        out = (ctypes.c_int * self.S)()
+        rc = self._L.h264mi_enc_nal_bytes(self._e, out)
+        if rc != 0:
+            raise RuntimeError(f'encoder kernels reported an error ({rc})')
+        return list(out)
+
+    def nal_ptr(self, s):
+        return self._L.h264mi_enc_nal_ptr(self._e, s)
+
+    def nal_ptrs(self):
+        return [self.nal_ptr(s) for s in range(self.S)]
+
+    def nal_bytes(self, s, size):
+        """Copy stream s's last NAL output to host bytes (testing / C-ABI style use)."""
+        import torch
+        buf = torch.empty(size, dtype=torch.uint8)
+        _hip_memcpy_d2h(buf.data_ptr(), self.nal_ptr(s), size)
+        return bytes(buf.numpy())
+
+    def nal_size_ptrs(self):
+        return [self._L.h264mi_enc_nal_size_dev(self._e, s) for s in range(self.S)]
+
+    def copy_nals(self, dst, slot, sizes=None):
+        """async device copy of every stream's NAL into dst[s*slot:(s+1)*slot] (uint8 CUDA tensor);
+        byte counts into sizes (int32 CUDA tensor of S) when given"""
+        sp = ctypes.c_void_p(sizes.data_ptr()) if sizes is not None else None
+        if self._L.h264mi_enc_copy_nals(self._e, ctypes.c_void_p(dst.data_ptr()), slot, sp) != 0:
+            raise RuntimeError('h264mi_enc_copy_nals failed')
+
+    def set_timing(self, on):
+        self._L.h264mi_enc_set_timing(self._e, 1 if on else 0)
+
+    def kernel_time(self):
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        if self._L.h264mi_enc_kernel_time(self._e, ctypes.byref(ms), ctypes.byref(n)) != 0:
+            raise RuntimeError('h264mi_enc_kernel_time failed')
+        return ms.value, n.value
+
+    def recon_ptr(self, s):
+        return self._L.h264mi_enc_recon_ptr(self._e, s)
+
+    def last_qp(self, s=0):
+        return self._L.h264mi_enc_last_qp(self._e, s)
+
+    def close(self):
+        if self._e:
+            self._L.h264mi_enc_destroy(self._e)
+            self._e = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BatchDecoder:
+    """S independent decoder instances (<= 32 per object) of one geometry; NAL units in HBM."""
+
+    def __init__(self, width, height, nstreams, stream=None):
+        import torch
+        self.w, self.h, self.S = width, height, nstreams
+        self._L = lib()
+        hs = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._d = self._L.h264mi_dec_create(width, height, nstreams, ctypes.c_void_p(hs))
+        if not self._d:
+            raise RuntimeError('h264mi_dec_create failed')
+        cw, ch = ctypes.c_int(), ctypes.c_int()
+        self._L.h264mi_dec_coded_size(self._d, ctypes.byref(cw), ctypes.byref(ch))
+        self.cw, self.ch = cw.value, ch.value
+
+    def decode(self, nal_ptrs, nal_sizes):
+        """nal_ptrs: device addresses (ints); nal_sizes: host ints (async)."""
+        ptrs = (ctypes.c_void_p * self.S)(*nal_ptrs)
+        sizes = (ctypes.c_int * self.S)(*nal_sizes)
+        if self._L.h264mi_dec_decode(self._d, ptrs, sizes) != 0:
+            raise RuntimeError('h264mi_dec_decode failed')
+
+    def decode_dev(self, nal_ptrs, size_ptrs):
+        """async; sizes read on the device from size_ptrs (e.g. BatchEncoder.nal_size_ptrs())"""
+        ptrs = (ctypes.c_void_p * self.S)(*nal_ptrs)
+        sz = (ctypes.c_void_p * self.S)(*size_ptrs)
+        if self._L.h264mi_dec_decode_dev(self._d, ptrs, sz) != 0:
+            raise RuntimeError('h264mi_dec_decode_dev failed')
+
+    def status(self):
+        got = (ctypes.c_int * self.S)()
+        rc = self._L.h264mi_dec_status(self._d, got)
+        return rc, list(got)
+
+    def picture_i420(self, s):
+        """Cropped tight I420 of stream s's last picture, as host bytes."""
+        import numpy as np
+        p = self._L.h264mi_dec_picture_ptr(self._d, s)
+        cw, ch = self.cw, self.ch
+        buf = np.empty(cw * ch * 3 // 2, np.uint8)
+        _hip_memcpy_d2h(buf.ctypes.data, p, buf.size)  # planes are contiguous: Y, U, V at coded size
+        y = buf[:cw * ch].reshape(ch, cw)[:self.h, :self.w]
+        u = buf[cw * ch:cw * ch * 5 // 4].reshape(ch // 2, cw // 2)[:self.h // 2, :self.w // 2]
+        v = buf[cw * ch * 5 // 4:].reshape(ch // 2, cw // 2)[:self.h // 2, :self.w // 2]
+        return np.concatenate([y.ravel(), u.ravel(), v.ravel()]).tobytes()
+
+    def close(self):
+        if self._d:
+            self._L.h264mi_dec_destroy(self._d)
+            self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _hip_memcpy_d2h(dst, src, n):
+    import torch
+    t = torch.cuda.current_stream()
+    t.synchronize()
+    hip = _hiprt()
+    rc = hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), ctypes.c_size_t(n), 2)
+    if rc != 0:
+        raise RuntimeError(f'hipMemcpy failed ({rc})')
+
+
+_hip = None
+
+
+def _hiprt():
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL('libamdhip64.so')
+        _hip.hipMemcpy.restype = ctypes.c_int
+    return _hip
+
+
+def version():
+    return lib().h264mi_version().decode()
