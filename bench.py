@@ -111,7 +111,10 @@ def main():
         host = np.stack([g.frame(t) for t in range(a.clip)])
         clip[:, i * F:(i + 1) * F].copy_(torch.from_numpy(host))
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    # one dedicated HIP stream orders encode -> decode -> NAL copy (a null handle would give the encoder
+    # and the decoder private streams of their own, with no ordering between them)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=stream)
     dec = h264mi.BatchDecoder(W, H, S, stream=stream)
     size_ptrs = enc.nal_size_ptrs()
@@ -140,16 +143,12 @@ def main():
     # ---- parity self-check before timing: decoder output == encoder reconstruction, every stream
     rc, got = dec.status()
     parity_ok = rc == 0 and all(got)
-    import ctypes
     for s in range(S):
-        cw, ch = dec.cw, dec.ch
-        a_ = torch.empty(cw * ch * 3 // 2, dtype=torch.uint8, device=dev)
-        b_ = torch.empty_like(a_)
-        hip = h264mi._hiprt()
-        hip.hipMemcpy(ctypes.c_void_p(a_.data_ptr()), ctypes.c_void_p(enc.recon_ptr(s)), ctypes.c_size_t(a_.numel()), 3)
-        hip.hipMemcpy(ctypes.c_void_p(b_.data_ptr()), ctypes.c_void_p(dec._L.h264mi_dec_picture_ptr(dec._d, s)),
-                      ctypes.c_size_t(b_.numel()), 3)
-        parity_ok = parity_ok and bool(torch.equal(a_, b_))
+        n = dec.cw * dec.ch * 3 // 2
+        a_, b_ = np.empty(n, np.uint8), np.empty(n, np.uint8)
+        h264mi._hip_memcpy_d2h(a_.ctypes.data, enc.recon_ptr(s), n)
+        h264mi._hip_memcpy_d2h(b_.ctypes.data, dec.picture_ptr(s), n)
+        parity_ok = parity_ok and bool(np.array_equal(a_, b_))
     # ---- timed region
     enc.set_timing(True)
     if dist:

@@ -15,6 +15,7 @@
 #ifndef H264MI_H
 #define H264MI_H
 #include <stddef.h>
+#include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -73,6 +74,8 @@ int h264mi_dec_decode(h264mi_decoder *d, const void *const *d_nal, const int *na
 int h264mi_dec_decode_dev(h264mi_decoder *d, const void *const *d_nal, const int *const *d_sizes);
 int h264mi_dec_sync(h264mi_decoder *d);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
+/* diagnostics: parse-kernel cycle counters, 16 per stream (enabled by env H264MI_PARSE_PROF=1) */
+int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
 void *h264mi_dec_stream(h264mi_decoder *d);

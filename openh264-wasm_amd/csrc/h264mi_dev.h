@@ -9,6 +9,11 @@
 #include "h264mi_types.h"
 
 #define DEV __device__ __forceinline__
+// Global-address-space pointers. Pointers loaded from descriptors are generic, and generic (flat)
+// accesses count against LGKM_CNT as well as VM_CNT: every LDS wait after a flat store would also
+// wait for the store to reach memory. Kernels that mix LDS traffic with global stores use these.
+#define GLOBAL __attribute__((address_space(1)))
+template <class T> __device__ __forceinline__ GLOBAL T *gbl(T *p) { return (GLOBAL T *)(uint64_t)p; }
 
 namespace h264mi {
 

@@ -14,7 +14,9 @@
 enum { MI_I4 = 0, MI_I16 = 1, MI_P16x16 = 2, MI_PSKIP = 3, MI_P16x8 = 4, MI_P8x16 = 5, MI_P8x8 = 6, MI_IPCM = 7 };
 
 // Per-macroblock side information (128 B). Written by the MB wavefront kernel (encoder) or the
-// parse kernel (decoder); read by CAVLC, reconstruction and deblocking.
+// parse kernel (decoder); read by CAVLC, reconstruction and deblocking. Decoder: the parse kernel
+// writes a raw record (i4mode = mode codes in decoding order, 0xff = predicted; mv = mvd at each
+// partition's first 4x4 block) and dec_recon_kernel rewrites it with resolved modes / vectors.
 struct MbInfo {
     uint8_t type, qp, cbp, i16mode;
     uint8_t cmode, qpc, pad0, pad1;

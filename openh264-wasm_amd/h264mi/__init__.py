@@ -61,6 +61,7 @@ def lib():
             'h264mi_dec_decode': (i, [vp, vp, vp]),
             'h264mi_dec_sync': (i, [vp]),
             'h264mi_dec_status': (i, [vp, vp]),
+            'h264mi_dec_parse_profile': (i, [vp, vp]),
             'h264mi_dec_picture_ptr': (vp, [vp, i]),
             'h264mi_dec_coded_size': (i, [vp, vp, vp]),
             'h264mi_dec_stream': (vp, [vp]),
@@ -279,6 +280,10 @@ class BatchDecoder:
         got = (ctypes.c_int * self.S)()
         rc = self._L.h264mi_dec_status(self._d, got)
         return rc, list(got)
+
+    def picture_ptr(self, s):
+        """Device pointer of stream s's last decoded picture (coded size, planes contiguous)."""
+        return self._L.h264mi_dec_picture_ptr(self._d, s)
 
     def picture_i420(self, s):
         """Cropped tight I420 of stream s's last picture, as host bytes."""

@@ -1,0 +1,43 @@
+// Latency microbenchmarks for the serial parse chain on gfx950 (one wave): dependent SALU ops,
+// dependent scalar loads from a constant table, dependent LDS read + readfirstlane, v_readlane.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+__constant__ uint32_t c_tab[4096];
+__global__ void k(uint64_t *out, uint32_t seed, int n) {
+    __shared__ uint32_t lds[4096];
+    for (int i = threadIdx.x; i < 4096; i += 64) lds[i] = (i * 2654435761u) & 4095;
+    __syncthreads();
+    uint32_t x = seed;
+    uint64_t t0 = clock64();
+    for (int i = 0; i < n; i++) {  // 8 dependent SALU ops per iteration
+        x = x * 3 + 1; x ^= x >> 7; x = x * 5 + 3; x ^= x >> 9; x += 11; x ^= x << 3; x = x * 7; x += i;
+    }
+    uint64_t t1 = clock64();
+    uint32_t y = __builtin_amdgcn_readfirstlane(x) & 4095;
+    for (int i = 0; i < n; i++) y = c_tab[y] & 4095;   // dependent scalar loads (K$)
+    uint64_t t2 = clock64();
+    uint32_t z = y;
+    for (int i = 0; i < n; i++) z = __builtin_amdgcn_readfirstlane(lds[z]) & 4095;  // LDS + readfirstlane
+    uint64_t t3 = clock64();
+    int v = threadIdx.x;
+    uint32_t w = z;
+    for (int i = 0; i < n; i++) w = (uint32_t)__builtin_amdgcn_readlane(v + (int)w, (int)(w & 63)) & 4095;
+    uint64_t t4 = clock64();
+    if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = t2 - t1; out[2] = t3 - t2; out[3] = t4 - t3; out[4] = x + y + z + w; }
+}
+int main() {
+    uint32_t h[4096];
+    for (int i = 0; i < 4096; i++) h[i] = (i * 40503u + 17) & 4095;
+    hipMemcpyToSymbol(HIP_SYMBOL(c_tab), h, sizeof(h));
+    uint64_t *d; hipMalloc(&d, 64);
+    uint64_t r[5];
+    int n = 10000;
+    for (int rep = 0; rep < 3; rep++) {
+        hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, d, 12345u, n);
+        hipMemcpy(r, d, 40, hipMemcpyDeviceToHost);
+        printf("per iter cycles: 8 SALU chain %.1f | s_load dep %.1f | lds+rfl dep %.1f | readlane dep %.1f\n",
+               r[0] / (double)n, r[1] / (double)n, r[2] / (double)n, r[3] / (double)n);
+    }
+    return 0;
+}
