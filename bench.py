@@ -33,6 +33,7 @@ def parse():
     ap.add_argument('--height', type=int, default=1080)
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
+    ap.add_argument('--group', type=int, default=8, help='frames per stream per decode call (frame-parallel entropy decoding)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=16)
     ap.add_argument('--cpu-procs', type=int, default=16)
@@ -111,34 +112,55 @@ def main():
         host = np.stack([g.frame(t) for t in range(a.clip)])
         clip[:, i * F:(i + 1) * F].copy_(torch.from_numpy(host))
     torch.cuda.synchronize()
-    # one dedicated HIP stream orders encode -> decode -> NAL copy (a null handle would give the encoder
-    # and the decoder private streams of their own, with no ordering between them)
-    stream = torch.cuda.Stream(device=dev)
-    torch.cuda.set_stream(stream)
-    enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=stream)
-    dec = h264mi.BatchDecoder(W, H, S, stream=stream)
-    size_ptrs = enc.nal_size_ptrs()
-    slot = 1 << 21
-    nal_buf = sizes_dev = None
+    # Two HIP streams: the encoder runs on `es`, the decoder on `ds`. The encoder codes a group of G
+    # frames per stream (P frames chain through its reconstruction, so it is sequential in time) and
+    # copies each frame's NAL units into a staging slot; the decoder then takes the whole group in one
+    # call, entropy-decoding all G x S slices concurrently before reconstructing them in order. Groups
+    # are double-buffered, so decoding group g overlaps encoding group g+1.
+    es = torch.cuda.Stream(device=dev)
+    ds = torch.cuda.Stream(device=dev)
+    G = a.group
+    enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
+    dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
+    slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
+    stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(2)]
+    stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(2)]
+    ev_enc = [torch.cuda.Event() for _ in range(2)]
+    ev_dec = [torch.cuda.Event() for _ in range(2)]
     if world > 1:
-        nal_buf = torch.empty(S * slot, dtype=torch.uint8, device=dev)
-        sizes_dev = torch.empty(S, dtype=torch.int32, device=dev)
-        if rank == 0:
-            gather_nals_to_rank0.rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev)
+        gather_nals_to_rank0.rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev) if rank == 0 else None
 
-    step_no = [0]
+    state = {'t': 0, 'g': 0}
 
-    def step():
-        t = step_no[0]
-        enc.encode(clip[t % a.clip])
-        dec.decode_dev(enc.nal_ptrs(), size_ptrs)
-        if world > 1:
-            enc.copy_nals(nal_buf, slot, sizes_dev)
-            gather_nals_to_rank0(dist, torch, nal_buf, sizes_dev, S, slot, rank, world)
-        step_no[0] += 1
+    def run_group(n):
+        """encode n frames of every stream, then decode them as one batch (async)"""
+        b = state['g'] & 1
+        with torch.cuda.stream(es):
+            es.wait_event(ev_dec[b])  # the decoder has finished reading this staging buffer
+            for j in range(n):
+                enc.encode(clip[state['t'] % a.clip])
+                enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
+                state['t'] += 1
+            ev_enc[b].record(es)
+        with torch.cuda.stream(ds):
+            ds.wait_event(ev_enc[b])
+            base = stage[b].data_ptr()
+            ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
+            szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
+            dec.decode_frames(ptrs, size_ptrs=szp)
+            if world > 1:
+                for j in range(n):
+                    gather_nals_to_rank0(dist, torch, stage[b][j], stage_sz[b][j], S, slot, rank, world)
+            ev_dec[b].record(ds)
+        state['g'] += 1
 
-    for _ in range(a.warmup):
-        step()
+    def run_steps(k):
+        while k > 0:
+            n = min(G, k)
+            run_group(n)
+            k -= n
+
+    run_steps(a.warmup)
     torch.cuda.synchronize()
     # ---- parity self-check before timing: decoder output == encoder reconstruction, every stream
     rc, got = dec.status()
@@ -155,8 +177,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    run_steps(a.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -67,14 +67,23 @@ int h264mi_enc_kernel_time(h264mi_encoder *e, double *ms_total, int *launches);
 
 typedef struct h264mi_decoder h264mi_decoder;
 h264mi_decoder *h264mi_dec_create(int width, int height, int nstreams, void *hip_stream);
+/* frame-batched decoder: each call may carry up to max_frames access units per stream. Their slices
+   are entropy-decoded concurrently (CAVLC parsing of a frame does not depend on other frames), then
+   reconstructed in order; after the call each stream's picture is that of its last frame. */
+h264mi_decoder *h264mi_dec_create_batch(int width, int height, int nstreams, int max_frames, void *hip_stream);
+int h264mi_dec_max_frames(h264mi_decoder *d);
 void h264mi_dec_destroy(h264mi_decoder *d);
 /* async; d_nal[s] / nal_bytes[s] (host array) per stream; a stream with nal_bytes 0 is skipped */
 int h264mi_dec_decode(h264mi_decoder *d, const void *const *d_nal, const int *nal_bytes);
 /* async; NAL sizes read from device memory (e.g. h264mi_enc_nal_size_dev): no host round trip */
 int h264mi_dec_decode_dev(h264mi_decoder *d, const void *const *d_nal, const int *const *d_sizes);
+/* async; nframes x nstreams access units, index f * nstreams + s; sizes from the host array
+   nal_bytes or, if it is NULL, from device pointers d_sizes */
+int h264mi_dec_decode_frames(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
+                             const int *const *d_sizes);
 int h264mi_dec_sync(h264mi_decoder *d);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
-/* diagnostics: parse-kernel cycle counters, 16 per stream (enabled by env H264MI_PARSE_PROF=1) */
+/* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream) (env H264MI_PARSE_PROF=1) */
 int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);

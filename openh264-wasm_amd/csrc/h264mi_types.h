@@ -77,18 +77,32 @@ struct EncDesc {
 };
 
 // Per-stream decoder state + buffers.
-struct DecState {
-    int32_t have_sps, have_pps;
-    int32_t mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4];
-    int32_t num_ref_default, pic_init_qp, cqp_off, dbk_ctrl, constrained_intra, redundant, bottom_field_poc, weighted;
-    int32_t has_ref;
-    int32_t got_pic;       // 1 if the last call produced a picture
-    int32_t slice_qp, dbk_idc;
-    int32_t err;
-    uint32_t epoch;
-    int32_t parity;        // pic[parity] = last output picture = reference for the next P slice
-    int32_t out_w, out_h;
+struct DecParams {          // SPS/PPS fields the slice layer needs (7.3.2.1, 7.3.2.2)
+    int32_t have_sps, have_pps, mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4];
+    int32_t nref, qp, cqp, dbkc, red, bfp;
 };
+struct DecState {
+    DecParams ps;          // parameter sets in effect when the next call starts
+    DecParams ps_next;     // written by the parse wave of a call's last frame, copied to ps after it
+    int32_t has_ref;       // a reference picture exists
+    int32_t got_pic;       // 1 if the frame being (or last) reconstructed produced a picture
+    int32_t dbk_idc;       // disable_deblocking_filter_idc of that frame
+    int32_t err;           // sticky: 3 = parse error, 2 = unsupported stream, 1 = wavefront abort
+    uint32_t epoch;        // hand-off tag, +1 per reconstructed picture
+    int32_t parity;        // pic[parity] = last output picture = reference for the next P slice
+};
+
+// One decode call processes up to B frames per stream. Entropy decoding of a frame does not depend
+// on other frames' pixels, so all B x S slices are parsed concurrently (one wave each); the
+// reconstruction / deblocking passes then run frame by frame.
+#define H264MI_MAX_NALS 32
+struct NalEnt { int32_t start, end, type; uint32_t stop; };  // header byte index, payload end, type, RBSP stop-bit index
+struct DecFrame {          // per (frame slot, stream): written by dec_scan_kernel and dec_parse_kernel
+    const uint8_t *nal;
+    int32_t nbytes, nnal, slice, err, got_pic, dbk_idc;
+    NalEnt e[H264MI_MAX_NALS];
+};
+struct DecInput { const uint8_t *nal; const int32_t *size_dev; int32_t size, pad; };  // one access unit
 
 struct DecDesc {
     uint8_t *cur[3];        // unfiltered reconstruction (coded size)
@@ -98,5 +112,6 @@ struct DecDesc {
     uint64_t *gran;
     uint64_t *dgran;
     DecState *st;
+    DecFrame *frm;          // this frame slot's NAL table and parse result
     int32_t cw, ch;         // allocated coded size
 };

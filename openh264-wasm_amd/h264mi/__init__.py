@@ -58,6 +58,9 @@ def lib():
             'h264mi_dec_decode_dev': (i, [vp, vp, vp]),
             'h264mi_dec_create': (vp, [i, i, i, vp]),
             'h264mi_dec_destroy': (None, [vp]),
+            'h264mi_dec_create_batch': (vp, [i, i, i, i, vp]),
+            'h264mi_dec_decode_frames': (i, [vp, i, vp, vp, vp]),
+            'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_decode': (i, [vp, vp, vp]),
             'h264mi_dec_sync': (i, [vp]),
             'h264mi_dec_status': (i, [vp, vp]),
@@ -248,14 +251,15 @@ class BatchEncoder:
 
 
 class BatchDecoder:
-    """S independent decoder instances (<= 32 per object) of one geometry; NAL units in HBM."""
+    """S independent decoder streams of one geometry; NAL units in HBM. max_frames > 1 enables
+    decode_frames(): several access units per stream per call, entropy-decoded concurrently."""
 
-    def __init__(self, width, height, nstreams, stream=None):
+    def __init__(self, width, height, nstreams, stream=None, max_frames=1):
         import torch
-        self.w, self.h, self.S = width, height, nstreams
+        self.w, self.h, self.S, self.B = width, height, nstreams, max_frames
         self._L = lib()
         hs = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        self._d = self._L.h264mi_dec_create(width, height, nstreams, ctypes.c_void_p(hs))
+        self._d = self._L.h264mi_dec_create_batch(width, height, nstreams, max_frames, ctypes.c_void_p(hs))
         if not self._d:
             raise RuntimeError('h264mi_dec_create failed')
         cw, ch = ctypes.c_int(), ctypes.c_int()
@@ -275,6 +279,17 @@ class BatchDecoder:
         sz = (ctypes.c_void_p * self.S)(*size_ptrs)
         if self._L.h264mi_dec_decode_dev(self._d, ptrs, sz) != 0:
             raise RuntimeError('h264mi_dec_decode_dev failed')
+
+    def decode_frames(self, nal_ptrs, nal_sizes=None, size_ptrs=None):
+        """async; n frames per stream: nal_ptrs[f * S + s] (device addresses), sizes either host ints
+        (nal_sizes) or device int32 addresses (size_ptrs). n <= max_frames."""
+        m = len(nal_ptrs)
+        assert m % self.S == 0 and m // self.S <= self.B
+        ptrs = (ctypes.c_void_p * m)(*nal_ptrs)
+        sizes = (ctypes.c_int * m)(*nal_sizes) if nal_sizes is not None else None
+        sp = (ctypes.c_void_p * m)(*size_ptrs) if size_ptrs is not None else None
+        if self._L.h264mi_dec_decode_frames(self._d, m // self.S, ptrs, sizes, sp) != 0:
+            raise RuntimeError('h264mi_dec_decode_frames failed')
 
     def status(self):
         got = (ctypes.c_int * self.S)()
