@@ -54,32 +54,6 @@ def cpu_baseline(a):
         return {'value': None, 'unit': 'frames/s', 'cores': procs, 'kind': 'port', 'sample': f'failed: {e!r}'}
 
 
-def gather_nals_to_rank0(dist, torch, nal_buf, sizes_dev, S, slot, rank, world):
-    """RCCL gatherv of this step's NAL units to rank 0: all_gather of the per-stream byte counts,
-    then exact-size point-to-point sends (batch_isend_irecv) of each stream's slot prefix.
-    Returns (on rank 0) a list of world*S byte counts; the payloads land in the receive buffer."""
-    sizes_all = torch.empty(world * S, dtype=torch.int32, device=sizes_dev.device)
-    dist.all_gather_into_tensor(sizes_all, sizes_dev)
-    sz = sizes_all.cpu().tolist()
-    ops = []
-    if rank == 0:
-        rx = gather_nals_to_rank0.rx
-        for r in range(1, world):
-            for s in range(S):
-                n = sz[r * S + s]
-                if n > 0:
-                    ops.append(dist.P2POp(dist.irecv, rx[(r * S + s) * slot:(r * S + s) * slot + n], r))
-    else:
-        for s in range(S):
-            n = sz[rank * S + s]
-            if n > 0:
-                ops.append(dist.P2POp(dist.isend, nal_buf[s * slot:s * slot + n], 0))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    return sz
-
-
 def main():
     a = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -96,6 +70,7 @@ def main():
     import torch
     import h264mi
     from h264mi.synth import SyntheticStream
+    from h264mi.shard import gather_nals_to_rank0, stream_ids
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -107,8 +82,8 @@ def main():
     F = W * H * 3 // 2
     # ---- synthetic clips, resident in HBM: clip[t] = S frames back to back
     clip = torch.empty((a.clip, S * F), dtype=torch.uint8, device=dev)
-    for i in range(S):
-        g = SyntheticStream(rank * S + i, W, H)
+    for i, sid in enumerate(stream_ids(rank, S)):
+        g = SyntheticStream(sid, W, H)
         host = np.stack([g.frame(t) for t in range(a.clip)])
         clip[:, i * F:(i + 1) * F].copy_(torch.from_numpy(host))
     torch.cuda.synchronize()
@@ -127,8 +102,7 @@ def main():
     stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(2)]
     ev_enc = [torch.cuda.Event() for _ in range(2)]
     ev_dec = [torch.cuda.Event() for _ in range(2)]
-    if world > 1:
-        gather_nals_to_rank0.rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev) if rank == 0 else None
+    rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
 
     state = {'t': 0, 'g': 0}
 
@@ -150,7 +124,7 @@ def main():
             dec.decode_frames(ptrs, size_ptrs=szp)
             if world > 1:
                 for j in range(n):
-                    gather_nals_to_rank0(dist, torch, stage[b][j], stage_sz[b][j], S, slot, rank, world)
+                    gather_nals_to_rank0(dist, torch, stage[b][j], stage_sz[b][j], S, slot, rank, world, rx)
             ev_dec[b].record(ds)
         state['g'] += 1
 

@@ -87,7 +87,7 @@ struct DecState {
     int32_t has_ref;       // a reference picture exists
     int32_t got_pic;       // 1 if the frame being (or last) reconstructed produced a picture
     int32_t dbk_idc;       // disable_deblocking_filter_idc of that frame
-    int32_t err;           // sticky: 3 = parse error, 2 = unsupported stream, 1 = wavefront abort
+    int32_t err;           // of the current/last frame: 3 = parse error, 2 = unsupported, 1 = wavefront abort
     uint32_t epoch;        // hand-off tag, +1 per reconstructed picture
     int32_t parity;        // pic[parity] = last output picture = reference for the next P slice
 };

@@ -1,0 +1,102 @@
+"""ctypes wrapper of the CPU oracle (oracle/h264o_api.h) -- TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import numpy as np
+
+vp = ctypes.c_void_p
+
+
+class Oracle:
+    def __init__(self, path):
+        L = ctypes.CDLL(path)
+        L.h264o_enc_create.restype = vp
+        L.h264o_enc_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.h264o_enc_destroy.argtypes = [vp]
+        L.h264o_enc_force_idr.argtypes = [vp]
+        L.h264o_enc_encode.argtypes = [vp, vp, vp, ctypes.c_int]
+        L.h264o_enc_recon.argtypes = [vp, vp]
+        L.h264o_enc_mbinfo.argtypes = [vp, vp]
+        L.h264o_enc_last_qp.argtypes = [vp]
+        L.h264o_rc_init_qp.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.h264o_rc_next_qp.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+        L.h264o_write_sps.restype = ctypes.c_size_t
+        L.h264o_write_sps.argtypes = [ctypes.c_int, ctypes.c_int, vp]
+        L.h264o_write_pps.restype = ctypes.c_size_t
+        L.h264o_write_pps.argtypes = [vp]
+        L.h264o_dec_create.restype = vp
+        L.h264o_dec_destroy.argtypes = [vp]
+        L.h264o_dec_decode.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp]
+        L.h264o_dec_mbinfo.argtypes = [vp, vp]
+        L.h264o_rgba_to_i420.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.h264o_i420_to_rgba.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
+        self.L = L
+
+    def encoder(self, w, h, br):
+        return OEnc(self.L, w, h, br)
+
+    def decoder(self):
+        return ODec(self.L)
+
+    def rgba_to_i420(self, rgba, w, h):
+        out = np.zeros(w * h * 3 // 2, np.uint8)
+        rgba = np.ascontiguousarray(rgba, np.uint8)
+        self.L.h264o_rgba_to_i420(rgba.ctypes.data, w, h, out.ctypes.data)
+        return out
+
+    def i420_to_rgba(self, i420, w, h):
+        i420 = np.ascontiguousarray(i420, np.uint8)
+        out = np.zeros(w * h * 4, np.uint8)
+        y = i420.ctypes.data
+        self.L.h264o_i420_to_rgba(y, y + w * h, y + w * h + (w // 2) * (h // 2), w, h, w, w // 2, out.ctypes.data)
+        return out
+
+
+class OEnc:
+    def __init__(self, L, w, h, br):
+        self.L, self.w, self.h = L, w, h
+        self.e = vp(L.h264o_enc_create(w, h, br))
+        assert self.e.value
+        self.buf = np.zeros(w * h * 4 + 65536, np.uint8)
+
+    def encode(self, i420):
+        i420 = np.ascontiguousarray(i420, np.uint8)
+        n = self.L.h264o_enc_encode(self.e, i420.ctypes.data, self.buf.ctypes.data, self.buf.size)
+        return self.buf[:n].tobytes()
+
+    def force_idr(self):
+        self.L.h264o_enc_force_idr(self.e)
+
+    def recon(self):
+        out = np.zeros(self.w * self.h * 3 // 2, np.uint8)
+        self.L.h264o_enc_recon(self.e, out.ctypes.data)
+        return out
+
+    def last_qp(self):
+        return self.L.h264o_enc_last_qp(self.e)
+
+    def __del__(self):
+        try:
+            self.L.h264o_enc_destroy(self.e)
+        except Exception:
+            pass
+
+
+class ODec:
+    def __init__(self, L):
+        self.L = L
+        self.d = vp(L.h264o_dec_create())
+        self.out = np.zeros(4096 * 2304 * 3 // 2, np.uint8)
+
+    def decode(self, nal):
+        """-> (rc, tight I420 bytes or None, w, h)"""
+        a = np.frombuffer(nal, np.uint8).copy() if len(nal) else np.zeros(1, np.uint8)
+        w, h = ctypes.c_int(0), ctypes.c_int(0)
+        rc = self.L.h264o_dec_decode(self.d, a.ctypes.data, len(nal), self.out.ctypes.data, ctypes.byref(w), ctypes.byref(h))
+        if rc == 1:
+            return rc, self.out[:w.value * h.value * 3 // 2].copy(), w.value, h.value
+        return rc, None, w.value, h.value
+
+    def __del__(self):
+        try:
+            self.L.h264o_dec_destroy(self.d)
+        except Exception:
+            pass

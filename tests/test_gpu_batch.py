@@ -1,0 +1,72 @@
+"""GPU: the device-resident batch API (many streams per launch, NAL units and sizes in HBM,
+frame-batched decoding) -- decoder picture == encoder reconstruction for every stream, stream
+bytes == oracle bytes, at the bench configuration's full 1080p size."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'tools'))
+
+
+@pytest.mark.parametrize('args', [
+    (176, 144, 300000, 2, 5, 1, 1),      # per-frame decode_dev
+    (176, 144, 300000, 3, 9, 0, 1),      # per-frame decode (host sizes)
+    (352, 288, 2000000, 2, 10, 1, 4),    # 4-frame batches, device sizes, ragged tail
+    (208, 120, 500000, 3, 7, 0, 3),      # cropped geometry, host sizes
+    (1920, 1080, 1000000, 4, 6, 1, 3),   # bench geometry
+], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3'])
+def test_batch_encode_decode(gpu_lib, args):
+    import batch_check
+    assert batch_check.main(*args)
+
+
+def test_color_host_entry_points(gpu_lib, oracle):
+    import ctypes
+    from golden.make_golden import rgba_frame
+    L = gpu_lib
+    for w, h in ((64, 48), (1920, 1080)):
+        rgba = rgba_frame(w, h, 3)
+        out = np.zeros(w * h * 3 // 2, np.uint8)
+        assert L.h264mi_rgba_to_i420_host(rgba.ctypes.data, w, h, out.ctypes.data) == 0
+        assert np.array_equal(out, oracle.rgba_to_i420(rgba, w, h))
+        yuv = np.random.default_rng(w).integers(0, 256, w * h * 3 // 2, dtype=np.uint8)
+        o2 = np.zeros(w * h * 4, np.uint8)
+        assert L.h264mi_i420_to_rgba_host(yuv.ctypes.data, w, h, o2.ctypes.data) == 0
+        assert np.array_equal(o2, oracle.i420_to_rgba(yuv, w, h))
+    assert L.h264mi_rgba_to_i420_host(rgba.ctypes.data, 63, 48, out.ctypes.data) == -1   # odd width
+
+
+def test_module_facade_replays_worker_sequence(gpu_lib, oracle):
+    """The Emscripten-Module-shaped facade, driven like encoder_worker.js / decoder_worker.js:
+    _malloc the frame, copy into HEAPU8, encode, read the out pointer with getValue, decode into a
+    heap buffer, compare with the oracle."""
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    w, h = 176, 144
+    M = h264mi.Module(heap_bytes=8 << 20)
+    init_encoder = M.cwrap('init_encoder', 'number', ['number', 'number', 'number'])
+    encode = M.cwrap('encode_frame_yuv_i420', None, ['number'] * 5)
+    init_decoder = M.cwrap('init_decoder', 'number', ['number'])
+    decode = M.cwrap('decode_frame_yuv_i420', None, ['number'] * 6)
+    assert init_encoder(w, h, 300000) == 0 and init_decoder(1) == 0
+    fsz = w * h * 3 // 2
+    src, outpp, outsz = M._malloc(fsz), M._malloc(4), M._malloc(4)
+    dst, wp, hp, nalp = M._malloc(fsz), M._malloc(4), M._malloc(4), M._malloc(1 << 20)
+    oe, od = oracle.encoder(w, h, 300000), oracle.decoder()
+    g = SyntheticStream(2, w, h)
+    for t in range(3):
+        f = np.ascontiguousarray(g.frame(t))
+        M.HEAPU8[src:src + fsz] = f.tobytes()
+        encode(src, w, h, outpp, outsz)
+        off, n = M.getValue(outpp, 'i32'), M.getValue(outsz, 'i32')
+        nal = bytes(M.HEAPU8[off:off + n])
+        assert nal == oe.encode(f)
+        M.HEAPU8[nalp:nalp + n] = nal
+        decode(1, nalp, n, dst, wp, hp)
+        assert (M.getValue(wp), M.getValue(hp)) == (w, h)
+        _, pic, _, _ = od.decode(nal)
+        assert bytes(M.HEAPU8[dst:dst + fsz]) == pic.tobytes()
