@@ -1,13 +1,16 @@
 #!/usr/bin/env python
 """bench.py -- BASELINE.json metric "1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264".
 
-One step = one frame of every stream this rank owns: GPU encode (libh264mi batch encoder, IPPP,
-intra period 0, wrapper parameters, 1 Mbps) immediately followed by the GPU decode of the NAL units
-it produced; at N > 1 the step also gathers every rank's NAL units to rank 0 over RCCL (config 5:
-32 streams = 4 per GPU x 8 GPUs). Inputs are synthetic 1080p I420 clips resident in HBM before the
-timed region. value = frames encoded+decoded by all ranks / max-over-ranks wall time.
+Workload (config 4's 8 concurrent 1080p streams per MI355X, doing the metric's encode+decode; at
+N > 1 weak-scaled with config 5's NAL gather): every rank owns S streams (default 8). One step =
+one frame of each of them: GPU encode (libh264mi batch encoder, IPPP, intra period 0, the wrapper's
+parameters, 1 Mbps) and GPU decode of exactly the NAL units produced, plus (N > 1) the gather of
+those NAL units to rank 0 over RCCL. Frames are encoded in groups of G and each group is decoded by
+one frame-batched call (concurrent entropy decoding), overlapped with encoding of the next group.
+Inputs are synthetic 1080p I420 clips resident in HBM before the timed region.
+value = frames encoded+decoded by all ranks / max-over-ranks wall time of K steps.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--group G]
   (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 """
 import argparse
@@ -26,18 +29,18 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=60)
-    ap.add_argument('--warmup', type=int, default=4)
-    ap.add_argument('--streams', type=int, default=4, help='streams per GPU (config 5: 32 streams / 8 GPUs)')
+    ap.add_argument('--steps', type=int, default=160)
+    ap.add_argument('--warmup', type=int, default=32)
+    ap.add_argument('--streams', type=int, default=8, help='streams per GPU (config 4: 8 concurrent 1080p streams on one MI355X)')
     ap.add_argument('--width', type=int, default=1920)
     ap.add_argument('--height', type=int, default=1080)
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
-    ap.add_argument('--group', type=int, default=8, help='frames per stream per decode call (frame-parallel entropy decoding)')
+    ap.add_argument('--group', type=int, default=16, help='frames per stream per decode call (frame-parallel entropy decoding)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=16)
     ap.add_argument('--cpu-procs', type=int, default=16)
-    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'pmc_enc_mb.json'))
+    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'round1', 'pmc_enc_mb.json'))
     return ap.parse_args()
 
 
@@ -190,8 +193,9 @@ def main():
             'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
             'config': {'workload': f'{W}x{H} IPPP encode+decode (intra period 0), {S} streams per GPU, '
-                                   f'{a.bitrate} bps, wrapper encoder params; NAL gather to rank 0 at N>1',
-                       'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate,
+                                   f'{a.bitrate} bps, wrapper encoder params, decode batches of {G} frames; '
+                                   f'NAL gather to rank 0 at N>1',
+                       'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G,
                        'parallelism': f'streams x{world} (weak)'},
             'roofline': {'bound': 'hbm', 'kernel': 'enc_mb_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBPS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
