@@ -85,6 +85,8 @@ int h264mi_dec_sync(h264mi_decoder *d);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
 /* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream) (env H264MI_PARSE_PROF=1) */
 int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);
+/* diagnostics: enc_mb_kernel section cycle counters, 16 totals (env H264MI_ENC_PROF=1) */
+int h264mi_enc_profile(h264mi_encoder *e, uint64_t *out);
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
 void *h264mi_dec_stream(h264mi_decoder *d);

@@ -13,6 +13,8 @@
 // accesses count against LGKM_CNT as well as VM_CNT: every LDS wait after a flat store would also
 // wait for the store to reach memory. Kernels that mix LDS traffic with global stores use these.
 #define GLOBAL __attribute__((address_space(1)))
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // plain vector types: HIP's uint2/uint4
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // classes cannot live in address space 1
 template <class T> __device__ __forceinline__ GLOBAL T *gbl(T *p) { return (GLOBAL T *)(uint64_t)p; }
 
 namespace h264mi {
@@ -147,17 +149,17 @@ DEV int group16_sum(int v) {
 // 8-byte {tag = epoch, payload} granules written by ONE sc1 (agent-scope atomic) store each and
 // polled with agent-scope relaxed loads (MI355X_MICROARCH.md § visibility, R2). Spins are bounded
 // and abort on a per-launch error word.
-DEV void gran_store(uint64_t *g, uint32_t epoch, uint32_t v) {
+template <class P> DEV void gran_store(P g, uint32_t epoch, uint32_t v) {
     __hip_atomic_store(g, ((uint64_t)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // lanes [0, n) each poll one granule; returns false on abort/timeout. Payload of lane's granule in *v.
-DEV bool gran_wait(const uint64_t *g, int n, uint32_t epoch, uint32_t *v, int32_t *abort_word) {
+template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, int32_t *abort_word) {
     int lane = threadIdx.x & 63;
     uint32_t val = 0;
     for (unsigned spins = 0;; spins++) {
         bool ok = true;
         if (lane < n) {
-            uint64_t x = __hip_atomic_load((uint64_t *)(g + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t x = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             val = (uint32_t)x;
             ok = (uint32_t)(x >> 32) == epoch;
         }

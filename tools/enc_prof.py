@@ -1,0 +1,34 @@
+"""enc_mb_kernel section profile (H264MI_ENC_PROF=1): S streams 1080p IPPP, prints cycles per MB
+per section summed over all waves, for I and P frames.   usage: enc_prof.py [w h br S nf]"""
+import os, sys
+os.environ['H264MI_ENC_PROF'] = '1'
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
+
+
+def main(w=1920, h=1080, br=1000000, S=8, nf=6):
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    gens = [SyntheticStream(s, w, h) for s in range(S)]
+    enc = h264mi.BatchEncoder(w, h, br, S)
+    L = h264mi.lib()
+    names = ['-', 'wait-above', 'loads+ctx', 'pskip-test', 'int-ME', 'subpel', 'intra-alt', 'p16-resid', 'I4-search',
+             'I-resid', 'outputs']
+    prev = np.zeros(16, np.uint64)
+    nmb = ((w + 15) // 16) * ((h + 15) // 16) * S
+    for t in range(nf):
+        frames = torch.from_numpy(np.concatenate([g.frame(t) for g in gens])).cuda()
+        enc.encode(frames)
+        sizes = enc.nal_sizes()
+        cur = np.zeros(16, np.uint64)
+        L.h264mi_enc_profile(enc._e, cur.ctypes.data)
+        d = (cur - prev).astype(np.float64) / nmb
+        prev = cur
+        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[1:11].sum():.0f} | ' +
+              ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(1, 11)), flush=True)
+
+
+if __name__ == '__main__':
+    main(*[int(x) for x in sys.argv[1:]])
