@@ -54,8 +54,9 @@ DEV QuantQP make_qqp(int qp) {
 }
 template <int POS> DEV int mf_of(const QuantQP &q) { return POSCLS[POS] == 0 ? q.mf0 : (POSCLS[POS] == 1 ? q.mf1 : q.mf2); }
 template <int POS> DEV int v_of(const QuantQP &q) { return POSCLS[POS] == 0 ? q.v0 : (POSCLS[POS] == 1 ? q.v1 : q.v2); }
+// 32-bit is exact here: |c| <= 9180 (4x4 transform of 8-bit residuals), mf <= 13107, f < 2^23
 DEV int quant1(int c, int mf, int qbits, int f) {
-    int l = (int)(((int64_t)iabs(c) * mf + f) >> qbits);
+    int l = (int)(((uint32_t)iabs(c) * (uint32_t)mf + (uint32_t)f) >> qbits);
     return c < 0 ? -l : l;
 }
 
@@ -123,8 +124,9 @@ DEV void dequant_block(const int16_t lv[16], const QuantQP &q, int c[16]) {
     DK(0) DK(1) DK(2) DK(3) DK(4) DK(5) DK(6) DK(7) DK(8) DK(9) DK(10) DK(11) DK(12) DK(13) DK(14) DK(15)
 #undef DK
 }
+// DC terms: |v| <= 32640 (luma, after >> 1) or 16320 (chroma): |v| * mf0 + 2f < 2^32
 DEV int quant_dc(int v, int mf0, int qbits, int f) {
-    int l = (int)(((int64_t)iabs(v) * mf0 + 2 * f) >> (qbits + 1));
+    int l = (int)(((uint32_t)iabs(v) * (uint32_t)mf0 + 2u * (uint32_t)f) >> (qbits + 1));
     return v < 0 ? -l : l;
 }
 // 8.5.10 luma DC scaling of one inverse-Hadamard output

@@ -80,11 +80,12 @@ struct EncDesc {
 struct DecParams {          // SPS/PPS fields the slice layer needs (7.3.2.1, 7.3.2.2)
     int32_t have_sps, have_pps, mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4];
     int32_t nref, qp, cqp, dbkc, red, bfp;
+    int32_t has_ref;       // parse-side view: a picture has been decoded before (P slices allowed)
 };
 struct DecState {
-    DecParams ps;          // parameter sets in effect when the next call starts
-    DecParams ps_next;     // written by the parse wave of a call's last frame, copied to ps after it
-    int32_t has_ref;       // a reference picture exists
+    DecParams ps;          // parameter sets of the picture last reconstructed (host reads crop)
+    DecParams psb[2];      // parse-stream chain: call k reads psb[k & 1], its last wave writes psb[~k & 1]
+    int32_t has_ref;       // reconstruction-side: a reference picture exists
     int32_t got_pic;       // 1 if the frame being (or last) reconstructed produced a picture
     int32_t dbk_idc;       // disable_deblocking_filter_idc of that frame
     int32_t err;           // of the current/last frame: 3 = parse error, 2 = unsupported, 1 = wavefront abort
@@ -92,9 +93,11 @@ struct DecState {
     int32_t parity;        // pic[parity] = last output picture = reference for the next P slice
 };
 
-// One decode call processes up to B frames per stream. Entropy decoding of a frame does not depend
-// on other frames' pixels, so all B x S slices are parsed concurrently (one wave each); the
-// reconstruction / deblocking passes then run frame by frame.
+// One decode call processes up to G frames per stream. Entropy decoding of a frame does not depend
+// on other frames' pixels, so all G x S slices are parsed concurrently (one wave each); the
+// reconstruction / deblocking passes then run frame by frame. Parsing runs on its own HIP stream
+// into one of two halves of 2G frame slots, so the parse of call k+1 overlaps the reconstruction of
+// call k.
 #define H264MI_MAX_NALS 32
 struct NalEnt { int32_t start, end, type; uint32_t stop; };  // header byte index, payload end, type, RBSP stop-bit index
 struct DecFrame {          // per (frame slot, stream): written by dec_scan_kernel and dec_parse_kernel
