@@ -37,6 +37,7 @@ def parse():
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
     ap.add_argument('--group', type=int, default=16, help='frames per stream per decode call (frame-parallel entropy decoding)')
+    ap.add_argument('--encode-only', action='store_true', help='diagnostic: skip decoding (not the metric)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=16)
     ap.add_argument('--cpu-procs', type=int, default=16)
@@ -119,6 +120,10 @@ def main():
                 enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
                 state['t'] += 1
             ev_enc[b].record(es)
+        if a.encode_only:
+            ev_dec[b].record(es)
+            state['g'] += 1
+            return
         with torch.cuda.stream(ds):
             ds.wait_event(ev_enc[b])
             base = stage[b].data_ptr()

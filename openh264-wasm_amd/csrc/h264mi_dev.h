@@ -147,6 +147,16 @@ DEV int group16_sum(int v) {
     return v;
 }
 
+// ---------------------------------------------------------------- intra-workgroup LDS hand-offs
+// __syncthreads() is a release/acquire fence at workgroup scope: it waits for every outstanding
+// global load AND store (vmcnt(0)) before the barrier. The wavefront kernels only hand data to each
+// other through LDS, so they use these instead: global traffic stays in flight across them.
+// lds_barrier: multi-wave workgroups (this wave's LDS operations done, then s_barrier).
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// wave_lds_sync: single-wave workgroups -- one wave's LDS requests complete in issue order, so
+// only the compiler must not move LDS accesses across this point.
+DEV void wave_lds_sync() { asm volatile("" ::: "memory"); }
+
 // ---------------------------------------------------------------- inter-workgroup hand-off (R2 granules)
 // 8-byte {tag = epoch, payload} granules written by ONE sc1 (agent-scope atomic) store each and
 // polled with agent-scope relaxed loads (MI355X_MICROARCH.md § visibility, R2). Spins are bounded
