@@ -129,7 +129,7 @@ def main():
             base = stage[b].data_ptr()
             ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
             szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
-            dec.decode_frames(ptrs, size_ptrs=szp)
+            dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])
             if world > 1:
                 for j in range(n):
                     gather_nals_to_rank0(dist, torch, stage[b][j], stage_sz[b][j], S, slot, rank, world, rx)

@@ -81,6 +81,11 @@ int h264mi_dec_decode_dev(h264mi_decoder *d, const void *const *d_nal, const int
    nal_bytes or, if it is NULL, from device pointers d_sizes */
 int h264mi_dec_decode_frames(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
                              const int *const *d_sizes);
+/* as h264mi_dec_decode_frames, but the inputs are ordered by ready_event (a hipEvent_t recorded by
+   the producer) instead of by the decoder's stream: entropy decoding of this call may then overlap
+   the reconstruction of the previous one. NULL = h264mi_dec_decode_frames. */
+int h264mi_dec_decode_frames_after(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
+                                   const int *const *d_sizes, void *ready_event);
 int h264mi_dec_sync(h264mi_decoder *d);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
 /* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream) (env H264MI_PARSE_PROF=1) */

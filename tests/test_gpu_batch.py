@@ -70,3 +70,58 @@ def test_module_facade_replays_worker_sequence(gpu_lib, oracle):
         assert (M.getValue(wp), M.getValue(hp)) == (w, h)
         _, pic, _, _ = od.decode(nal)
         assert bytes(M.HEAPU8[dst:dst + fsz]) == pic.tobytes()
+
+
+@pytest.mark.parametrize('use_event', [False, True], ids=['stream-ordered', 'ready-event'])
+def test_pipelined_two_stream_decode(gpu_lib, use_event):
+    """bench.py's pipeline without host synchronisation: the encoder codes groups of G frames on one
+    HIP stream and stages their NAL units; the decoder takes each group on a second stream (ordered
+    by wait_event, or by ready_event) while the next group is being encoded. After the last group
+    every stream's decoded picture must equal the encoder's reconstruction and no stream may report
+    an error (a parse of not-yet-written staging data fails one or the other)."""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    w, h, S, G, groups = 352, 288, 3, 4, 5
+    F = w * h * 3 // 2
+    clip = torch.empty((G * groups, S * F), dtype=torch.uint8, device='cuda')
+    for s in range(S):
+        g = SyntheticStream(10 + s, w, h)
+        clip[:, s * F:(s + 1) * F].copy_(torch.from_numpy(np.stack([g.frame(t) for t in range(G * groups)])))
+    torch.cuda.synchronize()
+    es, ds = torch.cuda.Stream(), torch.cuda.Stream()
+    enc = h264mi.BatchEncoder(w, h, 2000000, S, stream=es)
+    dec = h264mi.BatchDecoder(w, h, S, stream=ds, max_frames=G)
+    slot = 1 << 20
+    stage = [torch.empty((G, S * slot), dtype=torch.uint8, device='cuda') for _ in range(2)]
+    stage_sz = [torch.zeros((G, S), dtype=torch.int32, device='cuda') for _ in range(2)]
+    ev_enc = [torch.cuda.Event() for _ in range(2)]
+    ev_dec = [torch.cuda.Event() for _ in range(2)]
+    t = 0
+    for gi in range(groups):
+        b = gi & 1
+        with torch.cuda.stream(es):
+            es.wait_event(ev_dec[b])
+            for j in range(G):
+                enc.encode(clip[t])
+                enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
+                t += 1
+            ev_enc[b].record(es)
+        with torch.cuda.stream(ds):
+            ptrs = [stage[b].data_ptr() + j * S * slot + s * slot for j in range(G) for s in range(S)]
+            szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(G) for s in range(S)]
+            if use_event:
+                dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])
+            else:
+                ds.wait_event(ev_enc[b])
+                dec.decode_frames(ptrs, size_ptrs=szp)
+            ev_dec[b].record(ds)
+    torch.cuda.synchronize()
+    rc, got = dec.status()
+    assert rc == 0 and all(got)
+    n = dec.cw * dec.ch * 3 // 2
+    for s in range(S):
+        a_, b_ = np.empty(n, np.uint8), np.empty(n, np.uint8)
+        h264mi._hip_memcpy_d2h(a_.ctypes.data, enc.recon_ptr(s), n)
+        h264mi._hip_memcpy_d2h(b_.ctypes.data, dec.picture_ptr(s), n)
+        assert np.array_equal(a_, b_), f'stream {s}'
