@@ -16,6 +16,10 @@
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // plain vector types: HIP's uint2/uint4
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // classes cannot live in address space 1
 template <class T> __device__ __forceinline__ GLOBAL T *gbl(T *p) { return (GLOBAL T *)(uint64_t)p; }
+// Constant-address-space view of read-only launch data (descriptors, tables): uniform addresses then
+// load through the scalar cache into SGPRs instead of per-lane vector loads.
+#define CONSTANT __attribute__((address_space(4)))
+template <class T> __device__ __forceinline__ CONSTANT const T *cst(const T *p) { return (CONSTANT const T *)(uint64_t)p; }
 
 namespace h264mi {
 
@@ -34,6 +38,10 @@ __constant__ const uint8_t c_LAMBDA[52] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1
 
 DEV int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 DEV int clip1(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+// Clip1(x >> s) for byte-packed results. Clamp-first form: hipcc (ROCm 7.2, gfx950) selects
+// v_ashr_pk_u8_i32 for "shift, saturate, pack two bytes" and then assumes the instruction's upper 16
+// bits are zero, corrupting the neighbouring bytes.
+DEV int clip1_shr(int x, int s) { return min(max(x, 0), (256 << s) - 1) >> s; }
 DEV int iabs(int v) { return v < 0 ? -v : v; }
 DEV int median3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 DEV int ue_len(uint32_t v) { return 2 * (31 - __clz(v + 1)) + 1; }   // v < 2^31
@@ -136,16 +144,98 @@ DEV int luma_dc_scale(int f, const QuantQP &q) {
 }
 
 // ---------------------------------------------------------------- wave helpers (wave64)
-DEV int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+// A value every lane holds identically (read from LDS, reduced across lanes, ...) moved to an SGPR:
+// the compiler then treats what depends on it as uniform -- scalar branches and scalar table loads
+// instead of exec-mask juggling and per-lane global loads.
+DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// Cross-lane reductions on DPP (data-parallel primitives: an operand modifier of the VALU, no LDS
+// round trip; __shfl_* lowers to ds_bpermute, ~100+ cycles each on a dependent chain).
+// DPP controls: quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2), row_ror:4 = 0x124,
+// row_ror:8 = 0x128, row_half_mirror = 0x141 (lane i <-> 7-i within 8). All lanes read a valid source.
+template <int CTRL> DEV int dpp(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+DEV int lane_read(int v, int l) { return __builtin_amdgcn_readlane(v, l); }  // l uniform
+// total of each 16-lane row (lanes 16r..16r+15), in every lane of the row
 DEV int group16_sum(int v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v += dpp<0xB1>(v); v += dpp<0x4E>(v); v += dpp<0x124>(v); v += dpp<0x128>(v);
     return v;
 }
+DEV int group16_min(int v) {
+    v = min(v, dpp<0xB1>(v)); v = min(v, dpp<0x4E>(v)); v = min(v, dpp<0x124>(v)); v = min(v, dpp<0x128>(v));
+    return v;
+}
+// total of each 8-lane group, in every lane of the group
+DEV int group8_sum(int v) {
+    v += dpp<0xB1>(v); v += dpp<0x4E>(v); v += dpp<0x141>(v);
+    return v;
+}
+// wave64 total / minimum, returned uniform (SGPR)
+DEV int wave_sum(int v) {
+    v = group16_sum(v);
+    return lane_read(v, 0) + lane_read(v, 16) + lane_read(v, 32) + lane_read(v, 48);
+}
+DEV int wave_min(int v) {
+    v = group16_min(v);
+    return min(min(lane_read(v, 0), lane_read(v, 16)), min(lane_read(v, 32), lane_read(v, 48)));
+}
+
+// ---------------------------------------------------------------- lane-per-coefficient 4x4 transforms
+// A 4x4 block lives on 16 consecutive lanes, lane & 15 = 4r + c (raster). A 1-D pass along a row
+// reads the other three samples of its quad with quad_perm DPP; a pass along a column reads rows
+// (r+1)&3, (r+2)&3, (r+3)&3 with row_ror:12/8/4 (lane l <- lane (l - n) mod 16; checked on gfx950,
+// tools/micro/dpp.hip), so the column pass uses lane-constant coefficients in rotated order. The
+// coefficients of each pass are packed as 4 signed bytes in one VGPR (Xf), built once per kernel.
+DEV int sbyte(uint32_t p, int k) { return __builtin_amdgcn_sbfe((int)p, 8 * k, 8); }
+DEV int m24(int a, int b) { return __mul24(a, b); }  // v_mul_i32_i24: both operands |x| < 2^23
+// out = sum_k m_k x_(row r, column k)
+DEV int xf_row(int x, uint32_t m) {
+    return m24(sbyte(m, 0), dpp<0x00>(x)) + m24(sbyte(m, 1), dpp<0x55>(x)) + m24(sbyte(m, 2), dpp<0xAA>(x)) + m24(sbyte(m, 3), dpp<0xFF>(x));
+}
+// out = sum_j m_j x_(row (r+j)&3, column c)
+DEV int xf_col(int x, uint32_t m) {
+    return m24(sbyte(m, 0), x) + m24(sbyte(m, 1), dpp<0x12C>(x)) + m24(sbyte(m, 2), dpp<0x128>(x)) + m24(sbyte(m, 3), dpp<0x124>(x));
+}
+// inverse core transform pass (8.5.12.2): coefficient k enters halved where the matrix has 1/2;
+// sh holds one shift bit per k (same order as m)
+DEV int xf_row_inv(int x, uint32_t m, uint32_t sh) {
+    return m24(sbyte(m, 0), dpp<0x00>(x) >> (sh & 1)) + m24(sbyte(m, 1), dpp<0x55>(x) >> ((sh >> 1) & 1)) +
+           m24(sbyte(m, 2), dpp<0xAA>(x) >> ((sh >> 2) & 1)) + m24(sbyte(m, 3), dpp<0xFF>(x) >> ((sh >> 3) & 1));
+}
+DEV int xf_col_inv(int x, uint32_t m, uint32_t sh) {
+    return m24(sbyte(m, 0), x >> (sh & 1)) + m24(sbyte(m, 1), dpp<0x12C>(x) >> ((sh >> 1) & 1)) +
+           m24(sbyte(m, 2), dpp<0x128>(x) >> ((sh >> 2) & 1)) + m24(sbyte(m, 3), dpp<0x124>(x) >> ((sh >> 3) & 1));
+}
+constexpr int XF_FWD[4][4] = {{1, 1, 1, 1}, {2, 1, -1, -2}, {1, -1, -1, 1}, {1, -2, 2, -1}};   // 8.5 core transform
+constexpr int XF_HAD[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};   // 8-320 / 8-326
+constexpr int XF_INV[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};   // signs of 8-338..8-345
+constexpr int XF_INVSH[4][4] = {{0, 0, 0, 1}, {0, 1, 0, 0}, {0, 1, 0, 0}, {0, 0, 0, 1}};        // the 1/2 factors
+constexpr uint8_t XF_INVZZ[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};         // raster -> scan (Table 8-13)
+struct Xf {
+    uint32_t fr, fc, hr, hc, ir, ic;  // packed coefficient bytes per pass
+    uint32_t irs, ics;                // inverse shift bits per pass
+    int cls, zz;                      // quantiser position class (0: even/even, 1: odd/odd, 2: mixed), scan index
+};
+DEV Xf xf_consts(int pos) {
+    const int r = pos >> 2, c = pos & 3;
+    Xf x{};
+    for (int k = 0; k < 4; k++) {
+        const int j = (r + k) & 3;
+        x.fr |= (uint32_t)(XF_FWD[c][k] & 255) << (8 * k);
+        x.fc |= (uint32_t)(XF_FWD[r][j] & 255) << (8 * k);
+        x.hr |= (uint32_t)(XF_HAD[c][k] & 255) << (8 * k);
+        x.hc |= (uint32_t)(XF_HAD[r][j] & 255) << (8 * k);
+        x.ir |= (uint32_t)(XF_INV[c][k] & 255) << (8 * k);
+        x.ic |= (uint32_t)(XF_INV[r][j] & 255) << (8 * k);
+        x.irs |= (uint32_t)XF_INVSH[c][k] << k;
+        x.ics |= (uint32_t)XF_INVSH[r][j] << k;
+    }
+    x.cls = ((r | c) & 1) == 0 ? 0 : (((r & c) & 1) ? 1 : 2);
+    x.zz = XF_INVZZ[pos];
+    return x;
+}
+DEV int xf_fwd(int d, const Xf &x) { return xf_col(xf_row(d, x.fr), x.fc); }
+DEV int xf_had(int d, const Xf &x) { return xf_col(xf_row(d, x.hr), x.hc); }
+DEV int xf_inv(int w, const Xf &x) { return xf_col_inv(xf_row_inv(w, x.ir, x.irs), x.ic, x.ics); }
+DEV uint32_t popc(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
 
 // ---------------------------------------------------------------- intra-workgroup LDS hand-offs
 // __syncthreads() is a release/acquire fence at workgroup scope: it waits for every outstanding

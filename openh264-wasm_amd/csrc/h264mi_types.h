@@ -10,6 +10,14 @@
 #define H264MI_MB_SLOT_DWORDS 640      // per-MB CAVLC scratch (20480 bits; worst case < 17.6 kbit)
 #define H264MI_GRANULES_PER_MB 16      // row-to-row hand-off record (8-byte {tag,payload} granules)
 #define H264MI_DBK_GRANULES_PER_MB 24  // deblocking hand-off (luma rows 12..15, chroma rows 6..7)
+// Encoder reference planes are stored edge-padded (the picture's border samples replicated, the
+// half-sample planes computed from the replicated picture), so every motion-search access stays
+// inside the allocation without clamping. The column margins put the origin at 8 (mod 16) luma /
+// 4 (mod 8) chroma bytes, so that the window strips the MB kernel loads are 16- / 8-byte aligned.
+#define H264MI_LPADX 40
+#define H264MI_LPADY 32
+#define H264MI_CPADX 20
+#define H264MI_CPADY 16
 
 enum { MI_I4 = 0, MI_I16 = 1, MI_P16x16 = 2, MI_PSKIP = 3, MI_P16x8 = 4, MI_P8x16 = 5, MI_P8x8 = 6, MI_IPCM = 7 };
 
@@ -74,6 +82,11 @@ struct EncDesc {
     EncState *st;
     int32_t nal_cap;
     int32_t rbsp_cap;       // dwords
+    uint8_t *pl[4];         // padded luma reference planes at their origin: integer G, half-sample b
+                            // (horizontal), h (vertical), j (centre); rebuilt from dbk after each frame
+    uint8_t *plc[2];        // padded chroma reference planes (Cb, Cr) at their origin
+    int32_t ps, psc;        // row strides of pl / plc
+    int32_t pad3[2];
 };
 
 // Per-stream decoder state + buffers.

@@ -15,7 +15,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), 'lib', 'libh264mi.so')
+LIB_PATH = os.environ.get('H264MI_LIB') or os.path.join(os.path.dirname(_HERE), 'lib', 'libh264mi.so')  # env: diagnostics
 
 _lib = None
 
@@ -50,6 +50,7 @@ def lib():
             'h264mi_enc_frame_bytes': (ctypes.c_size_t, [vp]),
             'h264mi_enc_last_qp': (i, [vp, i]),
             'h264mi_enc_mbinfo': (i, [vp, i, vp]),
+            'h264mi_enc_ref_planes': (i, [vp, i, vp]),
             'h264mi_enc_stream': (vp, [vp]),
             'h264mi_enc_nal_size_dev': (vp, [vp, i]),
             'h264mi_enc_copy_nals': (i, [vp, vp, i, vp]),

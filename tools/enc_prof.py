@@ -15,7 +15,7 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
     enc = h264mi.BatchEncoder(w, h, br, S)
     L = h264mi.lib()
     names = ['-', 'wait-above', 'loads+ctx', 'pskip-test', 'int-ME', 'subpel', 'intra-alt', 'p16-resid', 'I4-search',
-             'I-resid', 'outputs']
+             'I-resid', 'outputs', 'F:pskip-pred', 'F:ME-first', 'F:satd-half', 'F:sel+satd-q', 'F:p16-pred']
     prev = np.zeros(16, np.uint64)
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * S
     for t in range(nf):
@@ -26,8 +26,8 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
         L.h264mi_enc_profile(enc._e, cur.ctypes.data)
         d = (cur - prev).astype(np.float64) / nmb
         prev = cur
-        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[1:11].sum():.0f} | ' +
-              ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(1, 11)), flush=True)
+        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[1:16].sum():.0f} | ' +
+              ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(1, 16) if d[k] > 0), flush=True)
 
 
 if __name__ == '__main__':
