@@ -87,6 +87,7 @@ struct EncDesc {
     uint8_t *plc[2];        // padded chroma reference planes (Cb, Cr) at their origin
     int32_t ps, psc;        // row strides of pl / plc
     int32_t pad3[2];
+    uint64_t *egran;        // MB -> deblocking hand-off, 128 granules per MB (deblock.inc DbkSrcGranules)
 };
 
 // Per-stream decoder state + buffers.
