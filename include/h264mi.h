@@ -42,6 +42,38 @@ void decode_frame_yuv_i420(int decoder_index, unsigned char *encoded_data, int s
 void free_buffer(void *ptr);
 
 /*
+ * Part 1b -- the same nine entry points on an explicit instance. The plain functions above act on
+ * one process-wide default instance (the wrapper's globals, openh264_wrapper.cpp:11-18). The
+ * reference runs one wasm instance per Worker, each with its own encoder and decoder_pool; a
+ * native host that loads this library once per process (the N-API addon) keeps
+ * that isolation by creating one instance per Worker. Same argument meaning and error behaviour.
+ */
+typedef struct h264mi_instance h264mi_instance;
+h264mi_instance *h264mi_instance_create(void);
+void h264mi_instance_destroy(h264mi_instance *inst);
+int h264mi_i_init_encoder(h264mi_instance *inst, int width, int height, int bitrate);
+void h264mi_i_force_key_frame(h264mi_instance *inst);
+void h264mi_i_deinit_decoder(h264mi_instance *inst, int decoder_index);
+int h264mi_i_init_decoder(h264mi_instance *inst, int decoder_index);
+void h264mi_i_encode_frame(h264mi_instance *inst, unsigned char *rgba_data, int width, int height, unsigned char **out_data,
+                           int *out_size);
+void h264mi_i_encode_frame_yuv_i420(h264mi_instance *inst, unsigned char *yuv_i420_data, int width, int height,
+                                    unsigned char **out_data, int *out_size);
+void h264mi_i_decode_frame_optimized(h264mi_instance *inst, int decoder_index, unsigned char *encoded_data, int size,
+                                     unsigned char *out_rgba_buffer, int *out_width, int *out_height);
+void h264mi_i_decode_frame_yuv_i420(h264mi_instance *inst, int decoder_index, unsigned char *encoded_data, int size,
+                                    unsigned char *out_yuv_buffer, int *out_width, int *out_height);
+/* as the two decoders above, with the output buffer's capacity: a picture that does not fit is
+   reported as "no picture" (zeroed width/height) instead of overrunning the buffer */
+void h264mi_i_decode_frame_optimized_cap(h264mi_instance *inst, int decoder_index, unsigned char *encoded_data, int size,
+                                         unsigned char *out_rgba_buffer, size_t out_cap, int *out_width, int *out_height);
+void h264mi_i_decode_frame_yuv_i420_cap(h264mi_instance *inst, int decoder_index, unsigned char *encoded_data, int size,
+                                        unsigned char *out_yuv_buffer, size_t out_cap, int *out_width, int *out_height);
+/* pinned (page-locked) host memory for a host's heap: host<->device copies of frames run at DMA rate */
+void *h264mi_host_alloc(size_t bytes);
+void h264mi_host_free(void *ptr);
+
+/*
  * Part 2 -- device-resident batch API (no reference counterpart: it is the MI355X-native way to
  * drive the same path for many independent streams whose frames/NAL units already live in HBM).
  * All "d_" pointers are device pointers; hip_stream is a hipStream_t (or NULL for an internal one).
