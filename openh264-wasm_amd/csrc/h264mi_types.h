@@ -131,4 +131,5 @@ struct DecDesc {
     DecState *st;
     DecFrame *frm;          // this frame slot's NAL table and parse result
     int32_t cw, ch;         // allocated coded size
+    uint64_t *egran;        // MB -> deblocking hand-off, 128 granules per MB (per stream)
 };
