@@ -37,6 +37,7 @@ def parse():
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
     ap.add_argument('--group', type=int, default=16, help='frames per stream per decode call (frame-parallel entropy decoding)')
+    ap.add_argument('--stages', type=int, default=3, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--encode-only', action='store_true', help='diagnostic: skip decoding (not the metric)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=16)
@@ -94,25 +95,28 @@ def main():
     # Two HIP streams: the encoder runs on `es`, the decoder on `ds`. The encoder codes a group of G
     # frames per stream (P frames chain through its reconstruction, so it is sequential in time) and
     # copies each frame's NAL units into a staging slot; the decoder then takes the whole group in one
-    # call, entropy-decoding all G x S slices concurrently before reconstructing them in order. Groups
-    # are double-buffered, so decoding group g overlaps encoding group g+1.
+    # call, entropy-decoding all G x S slices concurrently before reconstructing them in order. NB
+    # staging buffers keep NB groups in flight: encoding group g+1 overlaps the entropy decoding of
+    # group g and the reconstruction of group g-1 (with two buffers the encoder would wait for the
+    # reconstruction of g-1 before starting g+1, serialising encode -> parse -> reconstruct).
     es = torch.cuda.Stream(device=dev)
     ds = torch.cuda.Stream(device=dev)
     G = a.group
     enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
-    stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(2)]
-    stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(2)]
-    ev_enc = [torch.cuda.Event() for _ in range(2)]
-    ev_dec = [torch.cuda.Event() for _ in range(2)]
+    NB = max(2, a.stages)
+    stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
+    stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(NB)]
+    ev_enc = [torch.cuda.Event() for _ in range(NB)]
+    ev_dec = [torch.cuda.Event() for _ in range(NB)]
     rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
 
     state = {'t': 0, 'g': 0}
 
     def run_group(n):
         """encode n frames of every stream, then decode them as one batch (async)"""
-        b = state['g'] & 1
+        b = state['g'] % NB
         with torch.cuda.stream(es):
             es.wait_event(ev_dec[b])  # the decoder has finished reading this staging buffer
             for j in range(n):
