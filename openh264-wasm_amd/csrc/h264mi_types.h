@@ -90,6 +90,16 @@ struct EncDesc {
     uint64_t *egran;        // MB -> deblocking hand-off, 128 granules per MB (deblock.inc DbkSrcGranules)
 };
 
+// One stream's padded reference planes and the picture they are built from (enc_planes.inc).
+struct PlanesDesc {
+    const uint8_t *src[2][3];  // candidate source pictures (Y, U, V, coded size), src[*parity & 1] (src[0] if parity == nullptr)
+    const int32_t *parity;
+    const int32_t *active;     // nullptr, or build only if nonzero (decoder: a picture was produced)
+    uint8_t *pl[4];            // padded G, b, h, j planes at their origin (H264MI_LPADX/Y margins)
+    uint8_t *plc[2];           // padded Cb, Cr at their origin (H264MI_CPADX/Y margins)
+    int32_t ps, psc;
+};
+
 // Per-stream decoder state + buffers.
 struct DecParams {          // SPS/PPS fields the slice layer needs (7.3.2.1, 7.3.2.2)
     int32_t have_sps, have_pps, mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4];
@@ -132,4 +142,7 @@ struct DecDesc {
     DecFrame *frm;          // this frame slot's NAL table and parse result
     int32_t cw, ch;         // allocated coded size
     uint64_t *egran;        // MB -> deblocking hand-off, 128 granules per MB (per stream)
+    uint8_t *pl[4];         // padded planes of the reference picture (as the encoder's, per stream)
+    uint8_t *plc[2];
+    int32_t ps, psc;
 };
