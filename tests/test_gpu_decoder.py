@@ -113,3 +113,30 @@ def test_decoder_garbage_then_recovery(gpu_lib, oracle):
     gw, gh, got = gpu_decode(L, 7, nal, w, h)
     assert (gw, gh) == (w, h) and np.array_equal(got, pic)
     L.deinit_decoder(7)
+
+
+@pytest.mark.parametrize('max_mvd,dbk', [(24, 0), (160, 0), (400, 1)], ids=['mvd24', 'mvd160', 'mvd400-nodbk'])
+def test_long_vectors_vs_oracle(gpu_lib, oracle, max_mvd, dbk):
+    """Hand-built P pictures with arbitrary motion vectors (references far outside the picture and
+    outside the reconstruction kernel's LDS window) decode exactly as the oracle decoder does."""
+    import ctypes
+    import numpy as np
+    from h264mi.synth import SyntheticStream
+    from streamgen import p_frame
+    w, h = 176, 144
+    idr = oracle.encoder(w, h, 400000).encode(np.ascontiguousarray(SyntheticStream(3, w, h).frame(0)))
+    rng = np.random.default_rng(max_mvd)
+    units = [idr] + [p_frame(11, 9, t, 2 * t, rng, max_mvd=max_mvd, dbk_idc=dbk) for t in range(1, 6)]
+    od = oracle.decoder()
+    L = gpu_lib
+    assert L.init_decoder(5) == 0
+    out = np.zeros(w * h * 3 // 2, np.uint8)
+    gw, gh = ctypes.c_int(), ctypes.c_int()
+    for k, u in enumerate(units):
+        rc, ref, _, _ = od.decode(u)
+        assert rc == 1, k
+        buf = np.frombuffer(u, np.uint8).copy()
+        L.decode_frame_yuv_i420(5, buf.ctypes.data, len(u), out.ctypes.data, ctypes.byref(gw), ctypes.byref(gh))
+        assert (gw.value, gh.value) == (w, h), k
+        assert np.array_equal(out, ref), f'frame {k}'
+    L.deinit_decoder(5)
