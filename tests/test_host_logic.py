@@ -1,8 +1,10 @@
 """CPU: host-side pieces that need no GPU -- the synthetic input generator, the Emscripten-style
 Module arena, and the decoder-side NAL splitting used by the C-ABI geometry peek."""
 import hashlib
+import os
 
 import numpy as np
+import pytest
 
 
 def test_synthetic_stream_deterministic():
@@ -63,3 +65,21 @@ def test_module_cwrap_rejects_unexported(monkeypatch):
     m = _module(monkeypatch)
     with pytest.raises(KeyError):
         m.cwrap('not_a_wrapper_function', 'number', [])
+
+
+def test_code_object_has_no_ashr_pk(libpath, tmp_path):
+    """hipcc (ROCm 7.2, gfx950) mis-lowers "shift, saturate to u8, pack two bytes" to v_ashr_pk_u8_i32
+    with its upper 16 bits assumed zero; the sources use the clamp-first form. Guard:
+    the built gfx950 code object must not contain the instruction."""
+    import shutil
+    import subprocess
+    llvm = '/opt/rocm/lib/llvm/bin'
+    if not os.path.exists(os.path.join(llvm, 'llvm-objdump')):
+        pytest.skip('ROCm LLVM tools not installed')
+    fb, co = tmp_path / 'fb.bin', tmp_path / 'gfx950.co'
+    subprocess.run([os.path.join(llvm, 'llvm-objcopy'), '--dump-section', f'.hip_fatbin={fb}', libpath, str(tmp_path / 'x.so')], check=True)
+    subprocess.run([os.path.join(llvm, 'clang-offload-bundler'), '--unbundle', '--type=o', f'--input={fb}',
+                    '--targets=hipv4-amdgcn-amd-amdhsa--gfx950', f'--output={co}'], check=True)
+    dis = subprocess.run([os.path.join(llvm, 'llvm-objdump'), '-d', '--mcpu=gfx950', str(co)], capture_output=True, text=True, check=True).stdout
+    assert 'enc_mb_kernel' in dis
+    assert 'v_ashr_pk' not in dis

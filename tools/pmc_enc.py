@@ -17,7 +17,28 @@ def per_dispatch(d, counter, kernel='enc_mb_kernel'):
     return list(vals.values())
 
 
+def all_kernels(fd, wd):
+    """per-dispatch averages of every codec kernel: fetched (x2 corrected) and written MB"""
+    def table(d, counter):
+        f = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)[0]
+        acc = {}
+        for r in csv.DictReader(open(f)):
+            if r['Counter_Name'] != counter or 'h264mi::' not in r['Kernel_Name']:
+                continue
+            k = r['Kernel_Name'].split('h264mi::')[1].split('(')[0]
+            acc.setdefault(k, {}).setdefault(r['Dispatch_Id'], 0.0)
+            acc[k][r['Dispatch_Id']] += float(r['Counter_Value'])
+        return {k: sum(v.values()) / len(v) for k, v in acc.items()}
+    fe, wr = table(fd, 'FETCH_SIZE'), table(wd, 'WRITE_SIZE')
+    print('per dispatch: fetched MB (2 x FETCH_SIZE KiB) | written MB (WRITE_SIZE KiB)')
+    for k in sorted(fe, key=lambda k: -fe[k]):
+        print(f'  {k:28s} fetch {2 * fe[k] * 1024 / 1e6:10.2f} MB  write {wr.get(k, 0) * 1024 / 1e6:10.2f} MB')
+
+
 def main():
+    if '--all' in sys.argv:
+        all_kernels(sys.argv[1], sys.argv[2])
+        return
     fd, wd, out, w, h, s = sys.argv[1:7]
     fe, wr = per_dispatch(fd, 'FETCH_SIZE'), per_dispatch(wd, 'WRITE_SIZE')
     fkb, wkb = sum(fe) / len(fe), sum(wr) / len(wr)
