@@ -125,6 +125,8 @@ int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);
 /* diagnostics: the padded motion-search reference planes of a stream (luma G, b, h, j then Cb, Cr;
    sizes (cw+80)(ch+64) and (cw/2+40)(ch/2+32)), built from the last coded frame */
 int h264mi_enc_ref_planes(h264mi_encoder *e, int stream, void *host_out);
+/* diagnostics: dec_recon_kernel section cycle counters, 16 totals (env H264MI_RECON_PROF=1) */
+int h264mi_dec_recon_profile(h264mi_decoder *d, uint64_t *out);
 /* diagnostics: section cycle counters, 32 totals: 0..15 enc_mb_kernel, 16..31 the encoder's deblock_kernel (env H264MI_ENC_PROF=1) */
 int h264mi_enc_profile(h264mi_encoder *e, uint64_t *out);
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */

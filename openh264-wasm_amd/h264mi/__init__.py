@@ -62,6 +62,7 @@ def lib():
             'h264mi_dec_create_batch': (vp, [i, i, i, i, vp]),
             'h264mi_dec_decode_frames': (i, [vp, i, vp, vp, vp]),
             'h264mi_dec_decode_frames_after': (i, [vp, i, vp, vp, vp, vp]),
+            'h264mi_dec_recon_profile': (i, [vp, vp]),
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_decode': (i, [vp, vp, vp]),
             'h264mi_dec_sync': (i, [vp]),
