@@ -40,6 +40,7 @@ def parse():
     ap.add_argument('--stages', type=int, default=3, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--encode-only', action='store_true', help='diagnostic: skip decoding (not the metric)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--enc-priority', type=int, default=0, help='HIP stream priority of the encoder stream (-1 = high)')
     ap.add_argument('--cpu-frames', type=int, default=16)
     ap.add_argument('--cpu-procs', type=int, default=16)
     ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'round1', 'pmc_enc_mb.json'))
@@ -99,7 +100,7 @@ def main():
     # staging buffers keep NB groups in flight: encoding group g+1 overlaps the entropy decoding of
     # group g and the reconstruction of group g-1 (with two buffers the encoder would wait for the
     # reconstruction of g-1 before starting g+1, serialising encode -> parse -> reconstruct).
-    es = torch.cuda.Stream(device=dev)
+    es = torch.cuda.Stream(device=dev, priority=a.enc_priority)
     ds = torch.cuda.Stream(device=dev)
     G = a.group
     enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
