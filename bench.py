@@ -29,7 +29,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=160)
+    ap.add_argument('--steps', type=int, default=480)
     ap.add_argument('--warmup', type=int, default=32)
     ap.add_argument('--streams', type=int, default=8, help='streams per GPU (config 4: 8 concurrent 1080p streams on one MI355X)')
     ap.add_argument('--width', type=int, default=1920)

@@ -34,7 +34,8 @@ size_t h264o_write_pps(uint8_t *out);
 /* decoder: mirrors init_decoder / decode_frame_yuv_i420 */
 H264ODec *h264o_dec_create(void);
 void h264o_dec_destroy(H264ODec *d);
-/* returns 1 when a picture was output into out_i420 (tight, cropped), 0 otherwise, <0 on error */
+/* picture output into out_i420 (tight, cropped) -> 1: picture decoded, 2: damaged access unit concealed by a copy of the last picture (frame-copy
+ * error concealment), 0: no picture, -1: error with nothing to conceal */
 int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out_i420, int *w, int *h);
 void h264o_dec_mbinfo(const H264ODec *d, int32_t *out);
 

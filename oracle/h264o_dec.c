@@ -393,10 +393,23 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
     return 1;
 }
 
+/* tight cropped I420 copy of picture planes pic[] */
+static void emit_picture(const H264ODec *d, uint8_t *const pic[3], uint8_t *out, int *w, int *h) {
+    int W = d->cw - 2 * (d->crop[0] + d->crop[1]), H = d->ch - 2 * (d->crop[2] + d->crop[3]);
+    int x0 = 2 * d->crop[0], y0 = 2 * d->crop[2];
+    if (out) {
+        uint8_t *o = out;
+        for (int y = 0; y < H; y++, o += W) memcpy(o, pic[0] + (size_t)(y0 + y) * d->cw + x0, W);
+        for (int p = 1; p < 3; p++)
+            for (int y = 0; y < H / 2; y++, o += W / 2) memcpy(o, pic[p] + (size_t)(y0 / 2 + y) * (d->cw / 2) + x0 / 2, W / 2);
+    }
+    *w = W; *h = H;
+}
+/* returns 1: picture decoded, 2: damaged access unit concealed (frame copy), 0: no picture, -1: error */
 int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out, int *w, int *h) {
     *w = *h = 0;
     if (!d || !data || size <= 0) return -1;
-    int got_pic = 0, i = 0;
+    int got_pic = 0, damaged = 0, i = 0;
     while (i + 3 <= size) {
         /* find start code */
         int s = -1;
@@ -429,18 +442,17 @@ int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out, i
             if (rv == 1) got_pic = 1;
         }
         free(rb);
-        if (rv < 0) return -1;
+        if (rv < 0) { damaged = 1; break; }
+    }
+    if (damaged) {
+        /* ERROR_CON_FRAME_COPY (openh264_wrapper.cpp:269): a damaged access unit is concealed by a
+         * copy of the last picture, which stays the reference; with no earlier picture, no output */
+        if (!d->has_ref) return -1;
+        emit_picture(d, d->ref, out, w, h);
+        return 2;
     }
     if (!got_pic) return 0;
-    int W = d->cw - 2 * (d->crop[0] + d->crop[1]), H = d->ch - 2 * (d->crop[2] + d->crop[3]);
-    int x0 = 2 * d->crop[0], y0 = 2 * d->crop[2];
-    if (out) {
-        uint8_t *o = out;
-        for (int y = 0; y < H; y++, o += W) memcpy(o, d->cur[0] + (size_t)(y0 + y) * d->cw + x0, W);
-        for (int p = 1; p < 3; p++)
-            for (int y = 0; y < H / 2; y++, o += W / 2) memcpy(o, d->cur[p] + (size_t)(y0 / 2 + y) * (d->cw / 2) + x0 / 2, W / 2);
-    }
-    *w = W; *h = H;
+    emit_picture(d, d->cur, out, w, h);
     for (int p = 0; p < 3; p++) { uint8_t *t = d->ref[p]; d->ref[p] = d->cur[p]; d->cur[p] = t; }
     d->has_ref = 1;
     return 1;

@@ -91,7 +91,7 @@ class ODec:
         a = np.frombuffer(nal, np.uint8).copy() if len(nal) else np.zeros(1, np.uint8)
         w, h = ctypes.c_int(0), ctypes.c_int(0)
         rc = self.L.h264o_dec_decode(self.d, a.ctypes.data, len(nal), self.out.ctypes.data, ctypes.byref(w), ctypes.byref(h))
-        if rc == 1:
+        if rc in (1, 2):  # 2: damaged access unit concealed by a copy of the last picture
             return rc, self.out[:w.value * h.value * 3 // 2].copy(), w.value, h.value
         return rc, None, w.value, h.value
 

@@ -46,11 +46,12 @@ def nal(ref_idc, typ, rbsp):
     return bytes(out)
 
 
-def p_frame(mbw, mbh, frame_num, poc_lsb, rng, max_mvd=96, skip_prob=0.2, qp_delta=0, dbk_idc=0):
+def p_frame(mbw, mbh, frame_num, poc_lsb, rng, max_mvd=96, skip_prob=0.2, qp_delta=0, dbk_idc=0, first_mb=0):
     """One P access unit: each MB P_Skip (runs) with probability skip_prob, else P_L0_16x16 with a
-    random mvd in [-max_mvd, max_mvd] quarter samples and coded_block_pattern 0."""
+    random mvd in [-max_mvd, max_mvd] quarter samples and coded_block_pattern 0. first_mb > 0 makes
+    it the second slice of a two-slice picture (MBs first_mb..end)."""
     w = BitWriter()
-    w.ue(0)                 # first_mb_in_slice
+    w.ue(first_mb)          # first_mb_in_slice
     w.ue(5)                 # slice_type P (all slices of the picture P)
     w.ue(0)                 # pic_parameter_set_id
     w.u(frame_num & 0xffff, 16)
@@ -63,7 +64,7 @@ def p_frame(mbw, mbh, frame_num, poc_lsb, rng, max_mvd=96, skip_prob=0.2, qp_del
     if dbk_idc != 1:
         w.se(0); w.se(0)    # slice_alpha_c0_offset_div2, slice_beta_offset_div2
     run = 0
-    for _ in range(mbw * mbh):
+    for _ in range(mbw * mbh - first_mb):
         if rng.random() < skip_prob:
             run += 1
             continue

@@ -87,8 +87,9 @@ def test_decoder_pool_semantics(gpu_lib):
 
 
 def test_decoder_garbage_then_recovery(gpu_lib, oracle):
-    """damaged access units produce no picture (size 0, like a failed DecodeFrameNoDelay) and the
-    decoder resumes at the next IDR; the parse kernel must survive arbitrary payloads"""
+    """damaged access units produce no picture or the frame-copy concealment of the last picture
+    (ERROR_CON_FRAME_COPY) and the decoder resumes at the next IDR; the parse kernel must survive
+    arbitrary payloads"""
     from h264mi.synth import SyntheticStream
     w, h = 176, 144
     L = gpu_lib
@@ -113,6 +114,39 @@ def test_decoder_garbage_then_recovery(gpu_lib, oracle):
     gw, gh, got = gpu_decode(L, 7, nal, w, h)
     assert (gw, gh) == (w, h) and np.array_equal(got, pic)
     L.deinit_decoder(7)
+
+
+def test_decoder_frame_copy_concealment(gpu_lib, oracle):
+    """ERROR_CON_FRAME_COPY (openh264_wrapper.cpp:269): a damaged access unit -- here a truncated
+    P slice and a picture split into slices (outside the Baseline subset both decoders accept) --
+    outputs a copy of the last picture, which stays the reference, exactly as the oracle decoder
+    does; the following frames decode against it (drifted, identically in both decoders)."""
+    from h264mi.synth import SyntheticStream
+    from streamgen import p_frame
+    w, h = 176, 144
+    L = gpu_lib
+    assert L.init_decoder(9) == 0
+    oe, od = oracle.encoder(w, h, 300000), oracle.decoder()
+    g = SyntheticStream(4, w, h)
+    units = [oe.encode(np.ascontiguousarray(g.frame(t))) for t in range(6)]
+    units[2] = units[2][:len(units[2]) // 2]                                        # truncated slice
+    units[4] = p_frame(11, 9, 4, 8, np.random.default_rng(4), first_mb=33)          # second slice only
+    concealed = 0
+    for k, u in enumerate(units):
+        rc, pic, _, _ = od.decode(u)
+        gw, gh, got = gpu_decode(L, 9, u, w, h)
+        assert rc in (1, 2), k
+        concealed += rc == 2
+        assert (gw, gh) == (w, h) and np.array_equal(got, pic), f'frame {k} (oracle rc {rc})'
+    assert concealed == 2
+    L.deinit_decoder(9)
+    # nothing to conceal before the first picture: no output
+    assert L.init_decoder(9) == 0
+    od2 = oracle.decoder()
+    rc, _, _, _ = od2.decode(units[1])
+    assert rc <= 0
+    assert gpu_decode(L, 9, units[1], w, h)[:2] == (0, 0)
+    L.deinit_decoder(9)
 
 
 @pytest.mark.parametrize('max_mvd,dbk', [(24, 0), (160, 0), (400, 1)], ids=['mvd24', 'mvd160', 'mvd400-nodbk'])
