@@ -133,6 +133,28 @@ const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked 
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
 void *h264mi_dec_stream(h264mi_decoder *d);
 
+/*
+ * Device-resident NAL ring: the reference's SharedArrayBuffer frame pool
+ * (app.js:52-53, :292-310: FRAME_BUFFER_POOL_SIZE buffers of MAX_FRAME_SIZE bytes + {size, ref_count}
+ * per buffer) in HBM. Publishing follows encoder_worker.js:163-202 (size 0 -> nothing; larger than a
+ * slot -> dropped; slot ref_count > 0 -> dropped; else copy, size, ref_count = consumers); releasing
+ * follows decoder_worker.js:138-164 (Atomics.sub once per consumer). Decisions are taken on the device,
+ * in stream order, so neither side synchronises the host. Ticket t uses slot t % slots (the slot
+ * advances on a drop too, unlike the JS, so the host knows each ticket's slot without a round trip).
+ */
+typedef struct h264mi_nal_ring h264mi_nal_ring;
+h264mi_nal_ring *h264mi_ring_create(int slots, int slot_bytes);
+void h264mi_ring_destroy(h264mi_nal_ring *r);
+/* async on the encoder's stream: publish stream's last NAL output; returns the ticket, -1 on bad
+   arguments, -2 if ticket - 2*slots is not yet released by all its consumers */
+long long h264mi_ring_publish(h264mi_nal_ring *r, h264mi_encoder *e, int stream, int consumers);
+const void *h264mi_ring_nal_ptr(h264mi_nal_ring *r, long long ticket);  /* slot bytes (device) */
+const int *h264mi_ring_size_dev(h264mi_nal_ring *r, long long ticket);  /* device size word: bytes, 0 = dropped */
+/* async on hip_stream: one consumer is done with ticket (every consumer releases every ticket) */
+int h264mi_ring_release(h264mi_nal_ring *r, long long ticket, void *hip_stream);
+/* sync: counters, and ref_counts[slots] if non-NULL */
+int h264mi_ring_stats(h264mi_nal_ring *r, int *published, int *dropped_busy, int *dropped_size, int *ref_counts);
+
 /* edge colour conversions on the GPU, host buffers (openh264_wrapper.cpp:22-40 and :150-195) */
 int h264mi_rgba_to_i420_host(const unsigned char *rgba, int width, int height, unsigned char *out_i420);
 int h264mi_i420_to_rgba_host(const unsigned char *i420, int width, int height, unsigned char *out_rgba);

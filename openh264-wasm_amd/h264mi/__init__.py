@@ -74,6 +74,13 @@ def lib():
             'h264mi_dec_stream': (vp, [vp]),
             'h264mi_rgba_to_i420_host': (i, [vp, i, i, vp]),
             'h264mi_i420_to_rgba_host': (i, [vp, i, i, vp]),
+            'h264mi_ring_create': (vp, [i, i]),
+            'h264mi_ring_destroy': (None, [vp]),
+            'h264mi_ring_publish': (ctypes.c_longlong, [vp, vp, i, i]),
+            'h264mi_ring_nal_ptr': (vp, [vp, ctypes.c_longlong]),
+            'h264mi_ring_size_dev': (vp, [vp, ctypes.c_longlong]),
+            'h264mi_ring_release': (i, [vp, ctypes.c_longlong, vp]),
+            'h264mi_ring_stats': (i, [vp, vp, vp, vp, vp]),
             'h264mi_version': (cp, []),
         }
         for name, (res, args) in sig.items():
@@ -323,6 +330,56 @@ class BatchDecoder:
         if self._d:
             self._L.h264mi_dec_destroy(self._d)
             self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NalRing:
+    """Device-resident NAL ring: the reference's SharedArrayBuffer frame pool (app.js:52-53,
+    :292-310) with encoder_worker.js:163-202 publish and decoder_worker.js:138-164 release semantics,
+    decided on the device. Tickets are returned by publish(); decoders read nal_ptr(t)/size_ptr(t)
+    (size 0 = dropped, decoders skip it) and every consumer calls release(t) afterwards."""
+
+    def __init__(self, slots=40, slot_bytes=2 << 20):
+        self._L = lib()
+        self.slots, self.slot_bytes = slots, slot_bytes
+        self._r = self._L.h264mi_ring_create(slots, slot_bytes)
+        if not self._r:
+            raise RuntimeError('h264mi_ring_create failed')
+
+    def publish(self, enc, stream, consumers):
+        t = self._L.h264mi_ring_publish(self._r, enc._e, stream, consumers)
+        if t < 0:
+            raise RuntimeError(f'h264mi_ring_publish failed ({t})')
+        return t
+
+    def nal_ptr(self, t):
+        return self._L.h264mi_ring_nal_ptr(self._r, t)
+
+    def size_ptr(self, t):
+        return self._L.h264mi_ring_size_dev(self._r, t)
+
+    def release(self, t, stream=None):
+        import torch
+        hs = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        if self._L.h264mi_ring_release(self._r, t, ctypes.c_void_p(hs)) != 0:
+            raise RuntimeError('h264mi_ring_release failed')
+
+    def stats(self):
+        p, b, z = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        refs = (ctypes.c_int * self.slots)()
+        if self._L.h264mi_ring_stats(self._r, ctypes.byref(p), ctypes.byref(b), ctypes.byref(z), refs) != 0:
+            raise RuntimeError('h264mi_ring_stats failed')
+        return {'published': p.value, 'dropped_busy': b.value, 'dropped_size': z.value, 'ref_counts': list(refs)}
+
+    def close(self):
+        if self._r:
+            self._L.h264mi_ring_destroy(self._r)
+            self._r = None
 
     def __del__(self):
         try:
