@@ -40,6 +40,7 @@ def parse():
     ap.add_argument('--stages', type=int, default=3, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--encode-only', action='store_true', help='diagnostic: skip decoding (not the metric)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--lanes', type=int, default=1, help='encoder lanes: the streams split over this many encoders, each on its own HIP stream')
     ap.add_argument('--enc-priority', type=int, default=0, help='HIP stream priority of the encoder stream (-1 = high)')
     ap.add_argument('--cpu-frames', type=int, default=16)
     ap.add_argument('--cpu-procs', type=int, default=16)
@@ -100,16 +101,18 @@ def main():
     # staging buffers keep NB groups in flight: encoding group g+1 overlaps the entropy decoding of
     # group g and the reconstruction of group g-1 (with two buffers the encoder would wait for the
     # reconstruction of g-1 before starting g+1, serialising encode -> parse -> reconstruct).
-    es = torch.cuda.Stream(device=dev, priority=a.enc_priority)
+    L = a.lanes if a.lanes > 0 and S % a.lanes == 0 else 1
+    SL = S // L
+    ess = [torch.cuda.Stream(device=dev, priority=a.enc_priority) for _ in range(L)]
     ds = torch.cuda.Stream(device=dev)
     G = a.group
-    enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
+    encs = [h264mi.BatchEncoder(W, H, a.bitrate, SL, stream=ess[l]) for l in range(L)]
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
     stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(NB)]
-    ev_enc = [torch.cuda.Event() for _ in range(NB)]
+    ev_enc = [[torch.cuda.Event() for _ in range(L)] for _ in range(NB)]
     ev_dec = [torch.cuda.Event() for _ in range(NB)]
     rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
 
@@ -118,23 +121,31 @@ def main():
     def run_group(n):
         """encode n frames of every stream, then decode them as one batch (async)"""
         b = state['g'] % NB
-        with torch.cuda.stream(es):
-            es.wait_event(ev_dec[b])  # the decoder has finished reading this staging buffer
-            for j in range(n):
-                enc.encode(clip[state['t'] % a.clip])
-                enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
-                state['t'] += 1
-            ev_enc[b].record(es)
+        t0 = state['t']
+        for l in range(L):  # lane l codes streams [l*SL, (l+1)*SL) on its own HIP stream
+            es = ess[l]
+            with torch.cuda.stream(es):
+                es.wait_event(ev_dec[b])  # the decoder has finished reading this staging buffer
+                for j in range(n):
+                    enc = encs[l]
+                    enc.encode(clip[(t0 + j) % a.clip][l * SL * F:(l + 1) * SL * F])
+                    enc.copy_nals(stage[b][j][l * SL * slot:], slot, stage_sz[b][j][l * SL:])
+                ev_enc[b][l].record(es)
+        state['t'] = t0 + n
         if a.encode_only:
-            ev_dec[b].record(es)
+            with torch.cuda.stream(ds):
+                for l in range(L):
+                    ds.wait_event(ev_enc[b][l])
+                ev_dec[b].record(ds)
             state['g'] += 1
             return
         with torch.cuda.stream(ds):
-            ds.wait_event(ev_enc[b])
+            for l in range(L):
+                ds.wait_event(ev_enc[b][l])
             base = stage[b].data_ptr()
             ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
             szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
-            dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])
+            dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])  # parse waits for every lane
             if world > 1:
                 for j in range(n):
                     gather_nals_to_rank0(dist, torch, stage[b][j], stage_sz[b][j], S, slot, rank, world, rx)
@@ -155,11 +166,12 @@ def main():
     for s in range(S):
         n = dec.cw * dec.ch * 3 // 2
         a_, b_ = np.empty(n, np.uint8), np.empty(n, np.uint8)
-        h264mi._hip_memcpy_d2h(a_.ctypes.data, enc.recon_ptr(s), n)
+        h264mi._hip_memcpy_d2h(a_.ctypes.data, encs[s // SL].recon_ptr(s % SL), n)
         h264mi._hip_memcpy_d2h(b_.ctypes.data, dec.picture_ptr(s), n)
         parity_ok = parity_ok and bool(np.array_equal(a_, b_))
     # ---- timed region
-    enc.set_timing(True)
+    for enc in encs:
+        enc.set_timing(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -170,9 +182,11 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kms, nl = enc.kernel_time()
-    enc.set_timing(False)
-    sizes = enc.nal_sizes()
+    kt = [enc.kernel_time() for enc in encs]
+    kms, nl = sum(k[0] for k in kt), sum(k[1] for k in kt)
+    for enc in encs:
+        enc.set_timing(False)
+    sizes = [x for enc in encs for x in enc.nal_sizes()]
     if dist:
         tt = torch.tensor([elapsed, kms / max(nl, 1)], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -186,7 +200,7 @@ def main():
     value = frames / elapsed
     # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
     # (read source F + read reference F + write reconstruction F) for a P frame
-    alg_bytes = S * 3 * F
+    alg_bytes = SL * 3 * F
     achieved = alg_bytes / (kavg / 1e3) / 1e9
     traffic = None
     if os.path.exists(a.traffic):
@@ -204,8 +218,8 @@ def main():
             'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
             'config': {'workload': f'{W}x{H} IPPP encode+decode (intra period 0), {S} streams per GPU, '
                                    f'{a.bitrate} bps, wrapper encoder params, decode batches of {G} frames; '
-                                   f'NAL gather to rank 0 at N>1',
-                       'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G,
+                                   f'NAL gather to rank 0 at N>1' + (f'; {L} encoder lanes of {SL} streams' if L > 1 else ''),
+                       'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'encoder_lanes': L,
                        'parallelism': f'streams x{world} (weak)'},
             'roofline': {'bound': 'hbm', 'kernel': 'enc_mb_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBPS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,

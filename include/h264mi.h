@@ -118,6 +118,10 @@ int h264mi_dec_decode_frames(h264mi_decoder *d, int nframes, const void *const *
    the reconstruction of the previous one. NULL = h264mi_dec_decode_frames. */
 int h264mi_dec_decode_frames_after(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
                                    const int *const *d_sizes, void *ready_event);
+/* as above with several producers (e.g. encoder lanes on their own HIP streams): the inputs are
+   ordered after every one of the nevents hipEvent_t's; nevents 0 = h264mi_dec_decode_frames */
+int h264mi_dec_decode_frames_after_n(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
+                                     const int *const *d_sizes, void *const *ready_events, int nevents);
 int h264mi_dec_sync(h264mi_decoder *d);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
 /* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream) (env H264MI_PARSE_PROF=1) */

@@ -62,6 +62,7 @@ def lib():
             'h264mi_dec_create_batch': (vp, [i, i, i, i, vp]),
             'h264mi_dec_decode_frames': (i, [vp, i, vp, vp, vp]),
             'h264mi_dec_decode_frames_after': (i, [vp, i, vp, vp, vp, vp]),
+            'h264mi_dec_decode_frames_after_n': (i, [vp, i, vp, vp, vp, vp, i]),
             'h264mi_dec_recon_profile': (i, [vp, vp]),
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_decode': (i, [vp, vp, vp]),
@@ -294,15 +295,16 @@ class BatchDecoder:
     def decode_frames(self, nal_ptrs, nal_sizes=None, size_ptrs=None, ready_event=None):
         """async; n frames per stream: nal_ptrs[f * S + s] (device addresses), sizes either host ints
         (nal_sizes) or device int32 addresses (size_ptrs). n <= max_frames. Inputs are ordered after
-        the decoder's stream, or, if ready_event (a torch.cuda.Event recorded by the producer) is
-        given, after that event only."""
+        the decoder's stream, or, if ready_event (a torch.cuda.Event recorded by the producer, or a
+        list of them, one per producer stream) is given, after those events only."""
         m = len(nal_ptrs)
         assert m % self.S == 0 and m // self.S <= self.B
         ptrs = (ctypes.c_void_p * m)(*nal_ptrs)
         sizes = (ctypes.c_int * m)(*nal_sizes) if nal_sizes is not None else None
         sp = (ctypes.c_void_p * m)(*size_ptrs) if size_ptrs is not None else None
-        ev = ctypes.c_void_p(ready_event.cuda_event) if ready_event is not None else None
-        if self._L.h264mi_dec_decode_frames_after(self._d, m // self.S, ptrs, sizes, sp, ev) != 0:
+        evs = [] if ready_event is None else (list(ready_event) if isinstance(ready_event, (list, tuple)) else [ready_event])
+        ev = (ctypes.c_void_p * max(1, len(evs)))(*[e.cuda_event for e in evs])
+        if self._L.h264mi_dec_decode_frames_after_n(self._d, m // self.S, ptrs, sizes, sp, ev, len(evs)) != 0:
             raise RuntimeError('h264mi_dec_decode_frames failed')
 
     def status(self):
