@@ -14,9 +14,11 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
     gens = [SyntheticStream(s, w, h) for s in range(S)]
     enc = h264mi.BatchEncoder(w, h, br, S)
     L = h264mi.lib()
-    names = ['-', 'wait-above', 'loads+ctx', 'pskip-test', 'int-ME', 'subpel', 'intra-alt', 'p16-resid', 'I4-search',
+    names = ['row-start-wait', 'wait-above', 'loads+ctx', 'pskip-test', 'int-ME', 'subpel', 'intra-alt', 'p16-resid', 'I4-search',
              'I-resid', 'outputs', 'F:pskip-pred', 'F:ME-first', 'F:satd-half', 'F:sel+satd-q', 'F:p16-pred']
     prev = np.zeros(32, np.uint64)
+    enc.set_timing(True)
+    kprev = 0.0
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * S
     for t in range(nf):
         frames = torch.from_numpy(np.concatenate([g.frame(t) for g in gens])).cuda()
@@ -26,8 +28,11 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
         L.h264mi_enc_profile(enc._e, cur.ctypes.data)
         d = (cur - prev).astype(np.float64) / nmb
         prev = cur
-        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[1:16].sum():.0f} | ' +
-              ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(1, 16) if d[k] > 0), flush=True)
+        kms, _ = enc.kernel_time()
+        print(f'frame {t}: enc_mb {kms - kprev:.3f} ms (with profiling)', flush=True)
+        kprev = kms
+        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[0:16].sum():.0f} | ' +
+              ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(0, 16) if d[k] > 0), flush=True)
         dn = ['-', 'tile+prefetch', 'top-wait', 'bS+params', 'filter', 'stores+flush']
         print(f'   deblock cycles/MB: total {d[17:22].sum():.0f} | ' + ', '.join(f'{dn[k]} {d[16 + k]:.0f}' for k in range(1, 6)), flush=True)
 
