@@ -279,4 +279,21 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
     return true;
 }
 
+// one granule per lane, already loaded into x (e.g. one step ahead); lanes with need poll it until its
+// tag is epoch. Returns false on abort/timeout.
+template <class P> DEV bool gran_poll(P g, bool need, uint32_t epoch, uint64_t &x, int32_t *abort_word) {
+    for (unsigned spins = 0;; spins++) {
+        if (__all(!need || (uint32_t)(x >> 32) == epoch)) return true;
+        if ((spins & 255) == 255) {
+            int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ab || spins > (1u << 24)) {
+                if ((threadIdx.x & 63) == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (need) x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace h264mi
