@@ -1,19 +1,30 @@
 #!/usr/bin/env python
-"""bench.py -- BASELINE.json metric "1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264".
+"""bench.py -- BASELINE.json metric "1080p30 frames/sec encode+decode per GPU" on MI355X.
 
-Workload (config 4's 8 concurrent 1080p streams per MI355X, doing the metric's encode+decode; at
-N > 1 weak-scaled with config 5's NAL gather): every rank owns S streams (default 8). One step =
-one frame of each of them: GPU encode (libh264mi batch encoder, IPPP, intra period 0, the wrapper's
-parameters, 1 Mbps) and GPU decode of exactly the NAL units produced, plus (N > 1) the gather of
-those NAL units to rank 0 over RCCL. Frames are encoded in groups of G and each group is decoded by
-one frame-batched call (concurrent entropy decoding), overlapped with encoding of the next group.
-Inputs are synthetic 1080p I420 clips resident in HBM before the timed region.
+Parity: the GPU's NAL bytes and decoded pictures are checked against the oracle (oracle/, the CPU
+restatement of the reference path) on the bench's own geometry and bitrate before timing; parity
+with OpenH264 itself is unpinned. A failed check prints value null and exits 1.
+
+Default workload (the metric; at N > 1 also BASELINE.json configs[4]'s NAL gather): every rank owns
+S streams (default 8). One step = one frame of each of them: GPU encode (libh264mi batch encoder,
+IPPP, intra period 0, the wrapper's parameters, 1 Mbps) and GPU decode of exactly the NAL units
+produced, plus (N > 1) the gather of those NAL units to rank 0 over RCCL. Frames are encoded on one
+HIP stream and decoded in groups of G on another (entropy decoding of a group runs concurrently),
+overlapped with encoding. Inputs are synthetic I420 clips resident in HBM before the timed region.
 value = frames encoded+decoded by all ranks / max-over-ranks wall time of K steps.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--group G]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+Other BASELINE.json configs (one JSON line each, N = 1):
+  --config 2  1280x720, every frame IDR (force_key_frame), encode; S streams
+  --config 3  1920x1080 IPPP encode+decode, one stream
+  --config 4  1920x1080 decode only: 8 concurrent decoders of one 1080p stream (the app.js fan-out)
+  --config 5  1920x1080 IPPP encode+decode, 4 streams per GPU (32 over 8 GPUs), NAL gather at N > 1
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--streams S] [--group G]
+  --gpus N > 1 without a torch.distributed launcher: bench.py starts `torch.distributed.run` with N
+  ranks itself (a child process, before this process touches the GPU) and exits with its code.
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -24,60 +35,121 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = '1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264'
+PARITY_NOTE = 'NAL bytes and decoded pictures == oracle (CPU restatement) at this config; OpenH264 parity unpinned'
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=480)
-    ap.add_argument('--warmup', type=int, default=32)
-    ap.add_argument('--streams', type=int, default=8, help='streams per GPU (config 4: 8 concurrent 1080p streams on one MI355X)')
-    ap.add_argument('--width', type=int, default=1920)
-    ap.add_argument('--height', type=int, default=1080)
+    ap.add_argument('--steps', type=int, default=240)
+    ap.add_argument('--warmup', type=int, default=16)
+    ap.add_argument('--config', type=int, default=0, choices=[0, 2, 3, 4, 5], help='0 = the metric workload')
+    ap.add_argument('--streams', type=int, default=0, help='streams per GPU (default: 8; config 3: 1, config 5: 4)')
+    ap.add_argument('--width', type=int, default=0)
+    ap.add_argument('--height', type=int, default=0)
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
-    ap.add_argument('--group', type=int, default=16, help='frames per stream per decode call (frame-parallel entropy decoding)')
+    ap.add_argument('--group', type=int, default=4, help='frames per stream per decode call (frame-parallel entropy decoding)')
     ap.add_argument('--stages', type=int, default=3, help='NAL staging buffers (groups in flight between encoder and decoder)')
-    ap.add_argument('--encode-only', action='store_true', help='diagnostic: skip decoding (not the metric)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--lanes', type=int, default=1, help='encoder lanes: the streams split over this many encoders, each on its own HIP stream')
-    ap.add_argument('--enc-priority', type=int, default=0, help='HIP stream priority of the encoder stream (-1 = high)')
-    ap.add_argument('--cpu-frames', type=int, default=16)
-    ap.add_argument('--cpu-procs', type=int, default=16)
-    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'round1', 'pmc_enc_mb.json'))
-    return ap.parse_args()
+    ap.add_argument('--cpu-frames', type=int, default=7)
+    ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
+    ap.add_argument('--traffic', default='', help='JSON with hbm_bytes_per_launch measured by rocprofv3 for this exact config')
+    a = ap.parse_args()
+    if a.config == 2:
+        a.width, a.height = a.width or 1280, a.height or 720
+    a.width, a.height = a.width or 1920, a.height or 1080
+    a.streams = a.streams or {3: 1, 5: 4}.get(a.config, 8)
+    return a
 
 
-def cpu_baseline(a):
-    procs = min(a.cpu_procs, os.cpu_count() or 1)
+def relaunch(a):
+    """--gpus N > 1 outside a distributed launcher: run N ranks as a child torch.distributed.run
+    (nothing here has touched the GPU) and return its exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={a.gpus}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def cpu_baseline(a, mode):
     cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
-           '--bitrate', str(a.bitrate), '--frames', str(a.cpu_frames), '--procs', str(procs)]
+           '--bitrate', str(a.bitrate), '--frames', str(a.cpu_frames), '--mode', mode, '--hash', str(a.parity_frames)]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
-        line = [l for l in r.stdout.splitlines() if l.startswith('{')][-1]
-        d = json.loads(line)
-        return {k: d[k] for k in ('value', 'unit', 'cores', 'kind', 'sample')}
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])
+        return d
     except Exception as e:  # reported, never silently replaced
-        return {'value': None, 'unit': 'frames/s', 'cores': procs, 'kind': 'port', 'sample': f'failed: {e!r}'}
+        return {'value': None, 'unit': 'frames/s', 'cores': None, 'kind': 'port', 'sample': f'failed: {e!r}', 'parity_hashes': None}
+
+
+def gpu_parity(a, oracle_hashes, i_only=False):
+    """Stream 0's first frames on the GPU (fresh encoder + decoder, the bench's geometry and bitrate)
+    vs the oracle's sha256 of the same frames: NAL bytes and decoded pictures."""
+    import numpy as np
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    if not oracle_hashes:
+        return False, 'no oracle hashes (CPU baseline leg failed or skipped)'
+    g = SyntheticStream(0, a.width, a.height)
+    enc = h264mi.BatchEncoder(a.width, a.height, a.bitrate, 1)
+    dec = h264mi.BatchDecoder(a.width, a.height, 1)
+    ok = True
+    for t, want in enumerate(oracle_hashes):
+        f = torch.from_numpy(np.ascontiguousarray(g.frame(t))).cuda()
+        if i_only:
+            enc.force_idr(0)
+        enc.encode(f)
+        n = enc.nal_sizes()[0]
+        nal = enc.nal_bytes(0, n)
+        dec.decode([enc.nal_ptr(0)], [n])
+        rc, got = dec.status()
+        pic = dec.picture_i420(0) if rc == 0 and got[0] else b''
+        ok = ok and hashlib.sha256(nal).hexdigest() == want['nal'] and hashlib.sha256(pic).hexdigest() == want['pic']
+    enc.close()
+    dec.close()
+    return ok, f'stream 0 frames 0..{len(oracle_hashes) - 1}: ' + ('pass' if ok else 'FAIL')
+
+
+def timed(run_steps, K, W, dist, sync):
+    run_steps(W)
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run_steps(K)
+    sync()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
 
 
 def main():
     a = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if a.gpus > 1 and 'RANK' not in os.environ:
+        sys.exit(relaunch(a))
+    if a.gpus != world:
+        print(f'bench.py: --gpus {a.gpus} but WORLD_SIZE {world}', file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if a.gpus != world and world > 1:
-        print(f'warning: --gpus {a.gpus} but WORLD_SIZE {world}', file=sys.stderr)
-    # CPU baseline first, in child processes, before this process touches the GPU (rank 0, N = 1)
+    mode = {2: 'enc_i', 4: 'dec'}.get(a.config, 'encdec')
+    # CPU baseline + oracle parity hashes first, in child processes, before this process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a)
-
+        cpu = cpu_baseline(a, mode)
     import numpy as np
     import torch
     import h264mi
     from h264mi.synth import SyntheticStream
-    from h264mi.shard import gather_nals_to_rank0, stream_ids
+    from h264mi.shard import NalGather, stream_ids
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -85,70 +157,116 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
-    W, H, S = a.width, a.height, a.streams
+    parity_ok, parity_msg = True, 'skipped (--no-cpu-baseline or N > 1)'
+    if cpu is not None:
+        parity_ok, parity_msg = gpu_parity(a, cpu.get('parity_hashes'), i_only=a.config == 2)
+    W, H, S, G = a.width, a.height, a.streams, a.group
     F = W * H * 3 // 2
-    # ---- synthetic clips, resident in HBM: clip[t] = S frames back to back
+    sync = torch.cuda.synchronize
+    res = {}
+    if a.config == 4:
+        res = bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync)
+    else:
+        res = bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank)
+    parity_ok = parity_ok and res.pop('selfcheck_ok')
+    elapsed = res.pop('elapsed')
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+        ok = torch.tensor([1 if parity_ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity_ok = bool(ok.item())
+    frames = res.pop('frames_per_rank') * world
+    value = frames / elapsed
+    if rank == 0:
+        if cpu is not None:
+            cpu = {k: cpu.get(k) for k in ('value', 'unit', 'cores', 'kind', 'sample', 'value_1core')}
+        out = {
+            'metric': METRIC + ' (parity vs oracle; OpenH264 parity unpinned)',
+            'value': value if parity_ok else None, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+            'config': res.pop('config'),
+            'roofline': res.pop('roofline'),
+            'cpu_baseline': cpu,
+            'parity': {'vs_oracle': parity_msg, 'selfcheck': res.pop('selfcheck'), 'note': PARITY_NOTE},
+        }
+        out.update(res)
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+    if not parity_ok:
+        sys.exit(1)
+
+
+def roofline(kernel, alg_bytes, ms_total, launches, a, note=None):
+    kavg = ms_total / max(launches, 1)
+    achieved = alg_bytes / (kavg / 1e3) / 1e9 if kavg > 0 else 0.0
+    traffic = None
+    if a.traffic and os.path.exists(a.traffic):
+        tj = json.load(open(a.traffic))
+        if tj.get('width') == a.width and tj.get('height') == a.height and tj.get('streams') == a.streams and tj.get('kernel') == kernel:
+            traffic = tj.get('hbm_bytes_per_launch')
+    r = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+         'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic, 'alg_bytes_per_launch': alg_bytes, 'avg_launch_ms': kavg,
+         'launches': launches}
+    if note:
+        r['note'] = note
+    return r
+
+
+def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank):
+    """configs 0 (metric), 2 (I-only encode), 3 (one stream), 5 (4 streams): encode (+ decode)"""
+    W, H, S, G = a.width, a.height, a.streams, a.group
+    F = W * H * 3 // 2
+    i_only = a.config == 2
+    decode = not i_only
     clip = torch.empty((a.clip, S * F), dtype=torch.uint8, device=dev)
     for i, sid in enumerate(stream_ids(rank, S)):
         g = SyntheticStream(sid, W, H)
-        host = np.stack([g.frame(t) for t in range(a.clip)])
-        clip[:, i * F:(i + 1) * F].copy_(torch.from_numpy(host))
-    torch.cuda.synchronize()
-    # Two HIP streams: the encoder runs on `es`, the decoder on `ds`. The encoder codes a group of G
-    # frames per stream (P frames chain through its reconstruction, so it is sequential in time) and
-    # copies each frame's NAL units into a staging slot; the decoder then takes the whole group in one
-    # call, entropy-decoding all G x S slices concurrently before reconstructing them in order. NB
-    # staging buffers keep NB groups in flight: encoding group g+1 overlaps the entropy decoding of
-    # group g and the reconstruction of group g-1 (with two buffers the encoder would wait for the
-    # reconstruction of g-1 before starting g+1, serialising encode -> parse -> reconstruct).
-    L = a.lanes if a.lanes > 0 and S % a.lanes == 0 else 1
-    SL = S // L
-    ess = [torch.cuda.Stream(device=dev, priority=a.enc_priority) for _ in range(L)]
-    ds = torch.cuda.Stream(device=dev)
-    G = a.group
-    encs = [h264mi.BatchEncoder(W, H, a.bitrate, SL, stream=ess[l]) for l in range(L)]
-    dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
+        clip[:, i * F:(i + 1) * F].copy_(torch.from_numpy(np.stack([g.frame(t) for t in range(a.clip)])))
+    sync()
+    # The encoder codes frame t of all S streams on `es` (P frames chain through its reconstruction,
+    # so it is sequential in time) and copies each frame's NAL units to a staging slot; the decoder,
+    # on `ds`, takes G frames per call, entropy-decoding all G x S slices concurrently before
+    # reconstructing them in order. NB staging buffers keep NB groups in flight: encoding group g+1
+    # overlaps the entropy decoding of g and the reconstruction of g-1.
+    es, ds = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
+    dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G) if decode else None
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
     stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(NB)]
-    ev_enc = [[torch.cuda.Event() for _ in range(L)] for _ in range(NB)]
+    ev_enc = [torch.cuda.Event() for _ in range(NB)]
     ev_dec = [torch.cuda.Event() for _ in range(NB)]
-    rx = torch.empty(world * S * slot, dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
-
+    gather = NalGather(dist, torch, S, slot, G, rank, world, dev) if world > 1 else None
     state = {'t': 0, 'g': 0}
 
     def run_group(n):
-        """encode n frames of every stream, then decode them as one batch (async)"""
         b = state['g'] % NB
         t0 = state['t']
-        for l in range(L):  # lane l codes streams [l*SL, (l+1)*SL) on its own HIP stream
-            es = ess[l]
-            with torch.cuda.stream(es):
-                es.wait_event(ev_dec[b])  # the decoder has finished reading this staging buffer
-                for j in range(n):
-                    enc = encs[l]
-                    enc.encode(clip[(t0 + j) % a.clip][l * SL * F:(l + 1) * SL * F])
-                    enc.copy_nals(stage[b][j][l * SL * slot:], slot, stage_sz[b][j][l * SL:])
-                ev_enc[b][l].record(es)
+        with torch.cuda.stream(es):
+            es.wait_event(ev_dec[b])  # the decoder has finished with this staging buffer
+            if gather is not None and gather.done_event(b) is not None:
+                es.wait_event(gather.done_event(b))  # and the NAL gather's sends of it
+            for j in range(n):
+                if i_only:
+                    enc.force_idr(-1)
+                enc.encode(clip[(t0 + j) % a.clip])
+                enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
+            ev_enc[b].record(es)
         state['t'] = t0 + n
-        if a.encode_only:
-            with torch.cuda.stream(ds):
-                for l in range(L):
-                    ds.wait_event(ev_enc[b][l])
-                ev_dec[b].record(ds)
-            state['g'] += 1
-            return
         with torch.cuda.stream(ds):
-            for l in range(L):
-                ds.wait_event(ev_enc[b][l])
-            base = stage[b].data_ptr()
-            ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
-            szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
-            dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])  # parse waits for every lane
-            if world > 1:
-                for j in range(n):
-                    gather_nals_to_rank0(dist, torch, stage[b][j], stage_sz[b][j], S, slot, rank, world, rx)
+            ds.wait_event(ev_enc[b])
+            if decode:
+                base = stage[b].data_ptr()
+                ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
+                szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
+                dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])
+            if gather is not None:
+                gather.submit(stage[b], stage_sz[b], n, b)  # sizes gathered once per group; sends of the previous group
             ev_dec[b].record(ds)
         state['g'] += 1
 
@@ -157,80 +275,108 @@ def main():
             n = min(G, k)
             run_group(n)
             k -= n
+        if gather is not None:
+            gather.flush()
+
+    # warmup, then the self-check: decoder output == encoder reconstruction, every stream
+    run_steps(a.warmup)
+    sync()
+    selfcheck_ok = True
+    if decode:
+        rc, got = dec.status()
+        selfcheck_ok = rc == 0 and all(got)
+        n = dec.cw * dec.ch * 3 // 2
+        for s in range(S):
+            x, y = np.empty(n, np.uint8), np.empty(n, np.uint8)
+            h264mi._hip_memcpy_d2h(x.ctypes.data, enc.recon_ptr(s), n)
+            h264mi._hip_memcpy_d2h(y.ctypes.data, dec.picture_ptr(s), n)
+            selfcheck_ok = selfcheck_ok and bool(np.array_equal(x, y))
+    enc.set_timing(True)
+    if decode:
+        dec.set_timing(True)
+    elapsed = timed(run_steps, a.steps, 0, dist, sync)
+    ems, en = enc.kernel_time()
+    kern = {'enc_mb_kernel': {'avg_ms': ems / max(en, 1), 'launches': en}}
+    if decode:
+        rms, rn = dec.kernel_time(0)
+        pms, pn = dec.kernel_time(1)
+        kern['dec_recon_kernel'] = {'avg_ms': rms / max(rn, 1), 'launches': rn}
+        kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': S * G}
+    sizes = enc.nal_sizes()
+    # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
+    # (read source F + read reference F + write reconstruction F) for a P frame, 2F for an IDR
+    # 
+    alg = S * (2 if i_only else 3) * F
+    work = {0: 'IPPP encode+decode (intra period 0)', 2: 'I-only encode (force_key_frame before every frame)',
+            3: 'IPPP encode+decode (intra period 0), one stream', 5: 'IPPP encode+decode (intra period 0)'}[a.config]
+    cfg = {'workload': f'{W}x{H} {work}, {S} streams per GPU, {a.bitrate} bps, wrapper encoder params'
+                       + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
+           'baseline_config': {0: 'metric (configs[2] x 8 streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
+           'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'parallelism': f'streams x{world} (weak)'}
+    return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg,
+            'roofline': roofline('enc_mb_kernel', alg, ems, en, a), 'kernels': kern,
+            'selfcheck_ok': selfcheck_ok,
+            'selfcheck': ('decoder output == encoder reconstruction for every stream: ' + ('pass' if selfcheck_ok else 'FAIL'))
+            if decode else 'n/a (encode only)',
+            'last_nal_bytes': sizes}
+
+
+def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
+    """config 4: 8 concurrent decoders of one 1080p stream (app.js fans one encoded stream out to
+    numStreams decoders). The stream (stream 0, a.clip frames, IPPP) is encoded untimed; the timed
+    steps decode frame t in all S decoders (wrapping to the next IDR-started pass of the clip)."""
+    W, H, S, G = a.width, a.height, a.streams, a.group
+    F = W * H * 3 // 2
+    g = SyntheticStream(0, W, H)
+    enc = h264mi.BatchEncoder(W, H, a.bitrate, 1)
+    slot = 1 << 21
+    n = a.clip
+    units = torch.empty((n, slot), dtype=torch.uint8, device=dev)
+    usz = torch.zeros((n,), dtype=torch.int32, device=dev)
+    for t in range(n):
+        if t == 0:
+            enc.force_idr(0)
+        enc.encode(torch.from_numpy(np.ascontiguousarray(g.frame(t))).to(dev))
+        enc.copy_nals(units[t], slot, usz[t:t + 1])
+    sync()
+    nbytes = usz.cpu().tolist()
+    ds = torch.cuda.Stream(device=dev)
+    dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
+    state = {'t': 0}
+
+    def run_steps(k):
+        with torch.cuda.stream(ds):
+            while k > 0:
+                m = min(G, k, n - state['t'] % n)  # a call never wraps past the clip end (the next call starts at the IDR)
+                t0 = state['t'] % n
+                ptrs = [units[t0 + j].data_ptr() for j in range(m) for _ in range(S)]
+                szp = [usz[t0 + j:t0 + j + 1].data_ptr() for j in range(m) for _ in range(S)]
+                dec.decode_frames(ptrs, size_ptrs=szp)
+                state['t'] += m
+                k -= m
 
     run_steps(a.warmup)
-    torch.cuda.synchronize()
-    # ---- parity self-check before timing: decoder output == encoder reconstruction, every stream
+    sync()
     rc, got = dec.status()
-    parity_ok = rc == 0 and all(got)
-    for s in range(S):
-        n = dec.cw * dec.ch * 3 // 2
-        a_, b_ = np.empty(n, np.uint8), np.empty(n, np.uint8)
-        h264mi._hip_memcpy_d2h(a_.ctypes.data, encs[s // SL].recon_ptr(s % SL), n)
-        h264mi._hip_memcpy_d2h(b_.ctypes.data, dec.picture_ptr(s), n)
-        parity_ok = parity_ok and bool(np.array_equal(a_, b_))
-    # ---- timed region
-    for enc in encs:
-        enc.set_timing(True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_steps(a.steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kt = [enc.kernel_time() for enc in encs]
-    kms, nl = sum(k[0] for k in kt), sum(k[1] for k in kt)
-    for enc in encs:
-        enc.set_timing(False)
-    sizes = [x for enc in encs for x in enc.nal_sizes()]
-    if dist:
-        tt = torch.tensor([elapsed, kms / max(nl, 1)], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kavg = float(tt[0]), float(tt[1])
-        ok = torch.tensor([1 if parity_ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        parity_ok = bool(ok.item())
-    else:
-        kavg = kms / max(nl, 1)
-    frames = S * world * a.steps
-    value = frames / elapsed
-    # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
-    # (read source F + read reference F + write reconstruction F) for a P frame
-    alg_bytes = SL * 3 * F
-    achieved = alg_bytes / (kavg / 1e3) / 1e9
-    traffic = None
-    if os.path.exists(a.traffic):
-        try:
-            tj = json.load(open(a.traffic))
-            if tj.get('width') == W and tj.get('height') == H and tj.get('streams') == S:
-                traffic = tj.get('hbm_bytes_per_launch')
-        except Exception:
-            traffic = None
-    if rank == 0:
-        out = {
-            'metric': '1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264',
-            'value': value, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
-            'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
-            'config': {'workload': f'{W}x{H} IPPP encode+decode (intra period 0), {S} streams per GPU, '
-                                   f'{a.bitrate} bps, wrapper encoder params, decode batches of {G} frames; '
-                                   f'NAL gather to rank 0 at N>1' + (f'; {L} encoder lanes of {SL} streams' if L > 1 else ''),
-                       'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'encoder_lanes': L,
-                       'parallelism': f'streams x{world} (weak)'},
-            'roofline': {'bound': 'hbm', 'kernel': 'enc_mb_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBPS,
-                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
-                         'alg_bytes_per_launch': alg_bytes, 'avg_launch_ms': kavg},
-            'cpu_baseline': cpu,
-            'parity_selfcheck': 'decoder output == encoder reconstruction for every stream: ' + ('pass' if parity_ok else 'FAIL'),
-            'last_nal_bytes': sizes,
-        }
-        print(json.dumps(out))
-    if dist:
-        dist.destroy_process_group()
+    ok = rc == 0 and all(got)
+    pics = [dec.picture_i420(s) for s in range(S)]
+    ok = ok and all(p == pics[0] for p in pics)
+    dec.set_timing(True)
+    elapsed = timed(run_steps, a.steps, 0, None, sync)
+    rms, rn = dec.kernel_time(0)
+    pms, pn = dec.kernel_time(1)
+    alg = S * 2 * F  # decode P: read reference F + write picture F, per stream (SURVEY.md §8(d))
+    cfg = {'workload': f'{W}x{H} decode only: {S} concurrent decoders of one IPPP stream ({a.bitrate} bps, '
+                       f'{sum(nbytes) // n} B/frame mean), decode batches of {G} frames',
+           'baseline_config': 'configs[3]', 'width': W, 'height': H, 'decoders': S, 'bitrate': a.bitrate, 'group': G,
+           'parallelism': 'decoders x1'}
+    return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg,
+            'roofline': roofline('dec_recon_kernel', alg, rms, rn, a,
+                                 note='by GPU time dec_parse_kernel dominates: one wave per slice walks the serial CAVLC '
+                                      'chain (latency-bound, no meaningful HBM roofline)'),
+            'kernels': {'dec_recon_kernel': {'avg_ms': rms / max(rn, 1), 'launches': rn},
+                        'dec_parse_kernel': {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': S * G}},
+            'selfcheck_ok': ok, 'selfcheck': 'all decoders produce the same picture: ' + ('pass' if ok else 'FAIL')}
 
 
 if __name__ == '__main__':

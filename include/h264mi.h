@@ -123,6 +123,9 @@ int h264mi_dec_decode_frames_after(h264mi_decoder *d, int nframes, const void *c
 int h264mi_dec_decode_frames_after_n(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
                                      const int *const *d_sizes, void *const *ready_events, int nevents);
 int h264mi_dec_sync(h264mi_decoder *d);
+/* HIP-event timing of the decoder's kernels (bench.py): which 0 = dec_recon_kernel, 1 = dec_parse_kernel */
+int h264mi_dec_set_timing(h264mi_decoder *d, int enable);
+int h264mi_dec_kernel_time(h264mi_decoder *d, int which, double *ms_total, int *launches);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
 /* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream) (env H264MI_PARSE_PROF=1) */
 int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);

@@ -67,6 +67,8 @@ def lib():
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_decode': (i, [vp, vp, vp]),
             'h264mi_dec_sync': (i, [vp]),
+            'h264mi_dec_set_timing': (i, [vp, i]),
+            'h264mi_dec_kernel_time': (i, [vp, i, vp, vp]),
             'h264mi_dec_status': (i, [vp, vp]),
             'h264mi_dec_parse_profile': (i, [vp, vp]),
             'h264mi_enc_profile': (i, [vp, vp]),
@@ -306,6 +308,16 @@ class BatchDecoder:
         ev = (ctypes.c_void_p * max(1, len(evs)))(*[e.cuda_event for e in evs])
         if self._L.h264mi_dec_decode_frames_after_n(self._d, m // self.S, ptrs, sizes, sp, ev, len(evs)) != 0:
             raise RuntimeError('h264mi_dec_decode_frames failed')
+
+    def set_timing(self, on):
+        self._L.h264mi_dec_set_timing(self._d, 1 if on else 0)
+
+    def kernel_time(self, which=0):
+        """(total ms, launches) of dec_recon_kernel (which 0) or dec_parse_kernel (1) since set_timing"""
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        if self._L.h264mi_dec_kernel_time(self._d, which, ctypes.byref(ms), ctypes.byref(n)) != 0:
+            raise RuntimeError('h264mi_dec_kernel_time failed')
+        return ms.value, n.value
 
     def status(self):
         got = (ctypes.c_int * self.S)()

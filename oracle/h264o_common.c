@@ -513,11 +513,14 @@ static int compute_bs(const MBInfo *mp, int rp, const MBInfo *mq, int rq, int mb
     if (iabs(mp->mv[rp][0] - mq->mv[rq][0]) >= 4 || iabs(mp->mv[rp][1] - mq->mv[rq][1]) >= 4) return 1;
     return 0;
 }
-void deblock_frame(uint8_t *Y, uint8_t *U, uint8_t *V, int ys, int cs, const MBInfo *mbs, int mbw, int mbh) {
+/* cqp_off: chroma_qp_index_offset (8.7.2.2: QPc of each MB from its QPY + offset; I_PCM QPY = 0);
+ * off_a, off_b: FilterOffsetA/B = slice_alpha_c0_offset_div2 << 1, slice_beta_offset_div2 << 1 */
+void deblock_frame(uint8_t *Y, uint8_t *U, uint8_t *V, int ys, int cs, const MBInfo *mbs, int mbw, int mbh,
+                   int cqp_off, int off_a, int off_b) {
     for (int my = 0; my < mbh; my++)
         for (int mx = 0; mx < mbw; mx++) {
             const MBInfo *q = &mbs[my * mbw + mx];
-            int qpq = mb_qp_dbk(q), qcq = CHROMA_QP[clip3(0, 51, qpq)];
+            int qpq = mb_qp_dbk(q), qcq = CHROMA_QP[clip3(0, 51, qpq + cqp_off)];
             int bs[2][4][4]; /* [dir][edge][segment] */
             for (int e = 0; e < 4; e++)
                 for (int s = 0; s < 4; s++) {
@@ -533,17 +536,19 @@ void deblock_frame(uint8_t *Y, uint8_t *U, uint8_t *V, int ys, int cs, const MBI
                     const MBInfo *p = e == 0 ? (dir == 0 ? &mbs[my * mbw + mx - 1] : &mbs[(my - 1) * mbw + mx]) : q;
                     int qpp = mb_qp_dbk(p);
                     int qpav = (qpp + qpq + 1) >> 1;
-                    int alpha = DBK_ALPHA[qpav], beta = DBK_BETA[qpav];
+                    int ia = clip3(0, 51, qpav + off_a), ib = clip3(0, 51, qpav + off_b);
+                    int alpha = DBK_ALPHA[ia], beta = DBK_BETA[ib];
                     for (int i = 0; i < 16; i++) {
                         int b = bs[dir][e][i >> 2];
                         if (!b) continue;
                         uint8_t *ptr = dir == 0 ? &Y[(my * 16 + i) * ys + mx * 16 + 4 * e] : &Y[(my * 16 + 4 * e) * ys + mx * 16 + i];
-                        filter_line(ptr, dir == 0 ? 1 : ys, b, alpha, beta, b < 4 ? DBK_TC0[qpav][b - 1] : 0, 0);
+                        filter_line(ptr, dir == 0 ? 1 : ys, b, alpha, beta, b < 4 ? DBK_TC0[ia][b - 1] : 0, 0);
                     }
                     if (e & 1) continue; /* chroma edges at luma 0 and 8 only */
-                    int qcp = CHROMA_QP[clip3(0, 51, qpp)];
+                    int qcp = CHROMA_QP[clip3(0, 51, qpp + cqp_off)];
                     int qcav = (qcp + qcq + 1) >> 1;
-                    int ca = DBK_ALPHA[qcav], cb = DBK_BETA[qcav];
+                    int ica = clip3(0, 51, qcav + off_a), icb = clip3(0, 51, qcav + off_b);
+                    int ca = DBK_ALPHA[ica], cb = DBK_BETA[icb];
                     for (int pl = 0; pl < 2; pl++) {
                         uint8_t *P = pl ? V : U;
                         for (int i = 0; i < 8; i++) {
@@ -551,7 +556,7 @@ void deblock_frame(uint8_t *Y, uint8_t *U, uint8_t *V, int ys, int cs, const MBI
                             if (!b) continue;
                             int ce = e * 2; /* chroma edge offset: 0 or 4 */
                             uint8_t *ptr = dir == 0 ? &P[(my * 8 + i) * cs + mx * 8 + ce] : &P[(my * 8 + ce) * cs + mx * 8 + i];
-                            filter_line(ptr, dir == 0 ? 1 : cs, b, ca, cb, b < 4 ? DBK_TC0[qcav][b - 1] : 0, 1);
+                            filter_line(ptr, dir == 0 ? 1 : cs, b, ca, cb, b < 4 ? DBK_TC0[ica][b - 1] : 0, 1);
                         }
                     }
                 }

@@ -102,8 +102,8 @@ void mvp_part(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, i
               int pw, int ph, int shape, int out[2]);
 
 /* ---------------- deblocking ---------------- */
-void deblock_frame(uint8_t *y, uint8_t *u, uint8_t *v, int stride, int cstride, const MBInfo *mbs,
-                   int mbw, int mbh);   /* 8.7 */
+void deblock_frame(uint8_t *y, uint8_t *u, uint8_t *v, int stride, int cstride, const MBInfo *mbs, int mbw, int mbh,
+                  int cqp_off, int off_a, int off_b);   /* 8.7 */
 
 /* ---------------- CAVLC ---------------- */
 int nc_luma(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, int ras);

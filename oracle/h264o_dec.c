@@ -273,9 +273,13 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
     int dbk_idc = 0, dbk_a = 0, dbk_b = 0;
     if (d->dbk_ctrl) {
         dbk_idc = br_ue(r);
-        if (dbk_idc != 1) { dbk_a = br_se(r) * 2; dbk_b = br_se(r) * 2; }
+        if (dbk_idc > 2) return -1;
+        if (dbk_idc != 1) {
+            dbk_a = br_se(r) * 2; dbk_b = br_se(r) * 2;
+            if (dbk_a < -12 || dbk_a > 12 || dbk_b < -12 || dbk_b > 12) return -1;
+        }
     }
-    if (r->err || qp < 0 || qp > 51) return -1;
+    if (r->err || qp < 0 || qp > 51 || d->cqp_off < -12 || d->cqp_off > 12) return -1;
     int total = d->mbw * d->mbh, addr = 0, more = 1;
     while (more && addr < total) {
         if (st == 0) {
@@ -386,10 +390,9 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
     }
     if (addr != total) return -1;
     /* per-picture loop filter with the slice's parameters */
-    if (dbk_idc != 1) {
-        if (dbk_a || dbk_b || d->cqp_off || dbk_idc == 2) return -1; /* only default filter params in scope */
-        deblock_frame(d->cur[0], d->cur[1], d->cur[2], d->cw, d->cw / 2, d->mbs, d->mbw, d->mbh);
-    }
+    /* idc 2 (no filtering across slice edges) equals idc 0 for the single slice per picture in scope */
+    if (dbk_idc != 1)
+        deblock_frame(d->cur[0], d->cur[1], d->cur[2], d->cw, d->cw / 2, d->mbs, d->mbw, d->mbh, d->cqp_off, dbk_a, dbk_b);
     return 1;
 }
 

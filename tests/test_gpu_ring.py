@@ -171,3 +171,42 @@ def test_ring_fanout_zero_copy_decoders(gpu_lib, oracle):
         d.close()
     ring.close()
     enc.close()
+
+
+def test_ring_wraps_without_host_sync(gpu_lib):
+    """Publishes and releases enqueued back to back with NO host synchronisation, on a 2-slot ring
+    (ticket t + 4 reuses ticket t's size word): each publish that reuses a size word is ordered on
+    the device after every release of the ticket that last used it, so no release reads a word
+    that was already overwritten. Drops are timing-dependent (the JS pool's drop-when-busy), but
+    every ticket is either published or dropped exactly once and no reference count leaks."""
+    import torch
+    import h264mi
+    w, h, n, D = 176, 144, 14, 2
+    frames = _frames(w, h, n, 5)
+    es = torch.cuda.Stream()
+    dss = [torch.cuda.Stream() for _ in range(D)]
+    enc = h264mi.BatchEncoder(w, h, 300000, 1, stream=es)
+    decs = [h264mi.BatchDecoder(w, h, 1, stream=dss[k]) for k in range(D)]
+    ring = h264mi.NalRing(slots=2, slot_bytes=1 << 18)
+    torch.cuda.synchronize()
+    for t in range(n):
+        with torch.cuda.stream(es):
+            enc.encode(frames[t])
+            tk = ring.publish(enc, 0, D)
+            assert tk == t
+            ev = torch.cuda.Event()
+            ev.record(es)
+        for k in range(D):
+            with torch.cuda.stream(dss[k]):
+                dss[k].wait_event(ev)
+                decs[k].decode_frames([ring.nal_ptr(tk)], size_ptrs=[ring.size_ptr(tk)])
+                ring.release(tk, stream=dss[k])
+    torch.cuda.synchronize()
+    st = ring.stats()
+    assert st['published'] + st['dropped_busy'] + st['dropped_size'] == n
+    assert st['published'] >= 2 and st['dropped_size'] == 0
+    assert st['ref_counts'] == [0, 0]
+    for d in decs:
+        d.close()
+    ring.close()
+    enc.close()

@@ -1,5 +1,7 @@
-"""CPU: the N>1 path -- streams sharded across ranks, per-frame gather of staged NAL units to rank 0
-(all-gather of byte counts + exact-size point-to-point sends) -- on gloo with world_size 2."""
+"""CPU: the N>1 path -- streams sharded across ranks, gather of staged NAL units to rank 0 (all-gather
+of byte counts + exact-size point-to-point sends) -- on gloo: the per-frame helper at world_size 2,
+and bench.py's pipelined per-group NalGather at world_size 2 and 4 with real access units from the
+oracle encoder (ragged sizes: IDR + P frames of different streams)."""
 import os
 import socket
 
@@ -54,6 +56,86 @@ def test_gather_world2():
         p.start()
     for p in procs:
         p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _oracle_units(sid, nf, w=176, h=144):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
+    import numpy as np
+    from _oracle import Oracle
+    from h264mi.synth import SyntheticStream
+    O = Oracle(os.path.join(ROOT, 'oracle', 'build', 'libh264_oracle.so'))
+    e = O.encoder(w, h, 200000 + 50000 * sid)
+    g = SyntheticStream(sid, w, h)
+    return [e.encode(np.ascontiguousarray(g.frame(t))) for t in range(nf)]
+
+
+def _group_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from h264mi.shard import NalGather, stream_ids
+        S, G, slot, NB, nframes = 2, 3, 1 << 16, 3, 7  # groups of 3, 3, 1 frames
+        units = {sid: _oracle_units(sid, nframes) for sid in stream_ids(rank, S)}
+        gat = NalGather(dist, torch, S, slot, G, rank, world, None)
+        stage = [torch.zeros((G, S * slot), dtype=torch.uint8) for _ in range(NB)]
+        stage_sz = [torch.zeros((G, S), dtype=torch.int32) for _ in range(NB)]
+        got = []  # rank 0: per group, the received bytes of (rank, frame, stream)
+        t, g = 0, 0
+        while t < nframes:
+            n, b = min(G, nframes - t), g % NB
+            for j in range(n):
+                for i, sid in enumerate(stream_ids(rank, S)):
+                    u = units[sid][t + j]
+                    stage[b][j, i * slot:i * slot + len(u)] = torch.frombuffer(bytearray(u), dtype=torch.uint8)
+                    stage_sz[b][j, i] = len(u)
+            gat.submit(stage[b], stage_sz[b], n, b)
+            if rank == 0 and len(gat.received) > len(got):
+                got.append(_snapshot(gat, world, S, slot, gat.received[-1], len(gat.received[-1]) // (world * S)))
+            t += n
+            g += 1
+        gat.flush()
+        if rank == 0:
+            got.append(_snapshot(gat, world, S, slot, gat.received[-1], len(gat.received[-1]) // (world * S)))
+            everything = {sid: _oracle_units(sid, nframes) for sid in range(world * S)}
+            ok, t0 = len(got) == 3, 0
+            for grp in got:
+                n = len(grp) // (world * S)
+                for r in range(world):
+                    for j in range(n):
+                        for i in range(S):
+                            ok = ok and grp[(r * n + j) * S + i] == everything[r * S + i][t0 + j]
+                t0 += n
+            q.put(bool(ok and t0 == nframes))
+    finally:
+        dist.destroy_process_group()
+
+
+def _snapshot(gat, world, S, slot, sz, n):
+    return [bytes(gat.rx[u * slot:u * slot + sz[u]].numpy()) for u in range(world * n * S)]
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_group_gather_real_units(world):
+    """NalGather (bench.py's N > 1 path): per group of frames one size all-gather, the sends of each
+    group posted one group later; rank 0 receives every rank's access units byte for byte."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
 

@@ -1,34 +1,105 @@
-"""CPU baseline for bench.py: the oracle (CPU restatement of the reference path, oracle/) encoding
-and decoding the bench workload (synthetic 1080p IPPP) on host cores, one single-threaded stream per
-worker process (the wrapper runs OpenH264 single-threaded). Prints one JSON line.
-Run as a child process before the parent touches the GPU."""
-import argparse, ctypes, json, os, sys, time
+"""CPU baseline for bench.py: the oracle (oracle/, the CPU restatement of the reference path --
+TEST INFRASTRUCTURE, loaded here only as the baseline being timed and as the parity checker) run on
+host cores, one single-threaded stream per worker process (the wrapper runs OpenH264 single-threaded,
+SURVEY.md §2, openh264_wrapper.cpp:198-228 leaves threading off). Prints one JSON line.
+
+Modes (what one timed frame is, matching bench.py's configs):
+  encdec  1 IDR untimed, then P frames encoded + decoded        (metric, configs 3 and 5)
+  enc_i   every frame forced IDR, encoded                         (config 2)
+  dec     the stream is encoded untimed, then its P frames decoded (config 4)
+Also (--hash K): sha256 of the oracle's NAL bytes and decoded pictures of stream 0's first K frames,
+which bench.py compares with the GPU's bytes for the same frames (parity at the bench's own size).
+Run as a child process before the parent touches the GPU.
+"""
+import argparse, ctypes, hashlib, json, os, sys, time
 import multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def worker(args):
-    stream, w, h, bitrate, nframes = args
+    stream, w, h, bitrate, nframes, mode, nhash = args
     sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
     import numpy as np
     from h264mi.synth import SyntheticStream
     O = ctypes.CDLL(os.path.join(ROOT, 'oracle', 'build', 'libh264_oracle.so'))
     O.h264o_enc_create.restype = ctypes.c_void_p
     O.h264o_dec_create.restype = ctypes.c_void_p
+    vp = ctypes.c_void_p
     S = SyntheticStream(stream, w, h)
     frames = [np.ascontiguousarray(S.frame(t)) for t in range(nframes)]
-    e = ctypes.c_void_p(O.h264o_enc_create(w, h, bitrate))
-    d = ctypes.c_void_p(O.h264o_dec_create())
+    e = vp(O.h264o_enc_create(w, h, bitrate))
+    d = vp(O.h264o_dec_create())
     out = np.zeros(w * h * 4, np.uint8)
     pic = np.zeros(w * h * 3 // 2, np.uint8)
     W, H = ctypes.c_int(), ctypes.c_int()
+    hashes = []
+
+    def enc(f):
+        n = O.h264o_enc_encode(e, f.ctypes.data_as(vp), out.ctypes.data_as(vp), ctypes.c_int(out.size))
+        return n
+
+    def dec(buf, n):
+        return O.h264o_dec_decode(d, buf.ctypes.data_as(vp), ctypes.c_int(n), pic.ctypes.data_as(vp), ctypes.byref(W), ctypes.byref(H))
+
+    timed = 0.0
+    counted = 0
+    if mode == 'dec':
+        units = []
+        for f in frames:
+            n = enc(f)
+            units.append(out[:n].copy())
+        for t, u in enumerate(units):
+            t0 = time.perf_counter()
+            dec(u, u.size)
+            dt = time.perf_counter() - t0
+            if t > 0:
+                timed += dt; counted += 1
+            if t < nhash:
+                hashes.append({'nal': hashlib.sha256(u.tobytes()).hexdigest(), 'pic': hashlib.sha256(pic.tobytes()).hexdigest()})
+    else:
+        for t, f in enumerate(frames):
+            t0 = time.perf_counter()
+            if mode == 'enc_i':
+                O.h264o_enc_force_idr(e)
+            n = enc(f)
+            if mode == 'encdec':
+                dec(out, n)
+            dt = time.perf_counter() - t0
+            if mode == 'enc_i' or t > 0:
+                timed += dt; counted += 1
+            if t < nhash:
+                if mode != 'encdec':
+                    dec(out, n)
+                hashes.append({'nal': hashlib.sha256(out[:n].tobytes()).hexdigest(), 'pic': hashlib.sha256(pic.tobytes()).hexdigest()})
+    O.h264o_enc_destroy(e)
+    O.h264o_dec_destroy(d)
+    return timed, counted, hashes
+
+
+def host_cores():
+    """The CPU share this process may use: the affinity mask, capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU box sets 16 = its CPU share; nproc there shows the whole host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    omp = os.environ.get('OMP_NUM_THREADS')
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def run(procs, w, h, bitrate, frames, mode, nhash=0):
+    ctx = mp.get_context('spawn')
+    jobs = [(s, w, h, bitrate, frames, mode, nhash if s == 0 else 0) for s in range(procs)]
     t0 = time.perf_counter()
-    for f in frames:
-        n = O.h264o_enc_encode(e, f.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(out.size))
-        O.h264o_dec_decode(d, out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n), pic.ctypes.data_as(ctypes.c_void_p),
-                           ctypes.byref(W), ctypes.byref(H))
-    return time.perf_counter() - t0
+    if procs == 1:
+        res = [worker(jobs[0])]
+    else:
+        with ctx.Pool(procs) as pool:
+            res = pool.map(worker, jobs)
+    wall = time.perf_counter() - t0
+    counted = sum(r[1] for r in res)
+    busy = max(r[0] for r in res)
+    return counted / busy, counted, busy, wall, res[0][2]
 
 
 def main():
@@ -36,20 +107,19 @@ def main():
     ap.add_argument('--width', type=int, default=1920)
     ap.add_argument('--height', type=int, default=1080)
     ap.add_argument('--bitrate', type=int, default=1000000)
-    ap.add_argument('--frames', type=int, default=16)
-    ap.add_argument('--procs', type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument('--frames', type=int, default=7, help='frames per process (the first, IDR, is untimed except in enc_i)')
+    ap.add_argument('--mode', default='encdec', choices=['encdec', 'enc_i', 'dec'])
+    ap.add_argument('--procs', type=int, default=0, help='0: the host CPU share (host_cores())')
+    ap.add_argument('--hash', type=int, default=0, help='sha256 of stream 0 frames 0..K-1 (NAL bytes, decoded picture)')
     a = ap.parse_args()
-    ctx = mp.get_context('spawn')
-    t0 = time.perf_counter()
-    with ctx.Pool(a.procs) as pool:
-        times = pool.map(worker, [(s, a.width, a.height, a.bitrate, a.frames) for s in range(a.procs)])
-    wall = time.perf_counter() - t0
-    frames = a.procs * a.frames
-    busy = max(times)
-    print(json.dumps({'value': frames / busy, 'unit': 'frames/s', 'cores': a.procs, 'kind': 'port',
-                      'sample': f'{a.procs} procs x 1 stream x {a.frames} frames {a.width}x{a.height} IPPP '
-                                f'(1 IDR + {a.frames - 1} P), oracle encode+decode, timed per process (max)',
-                      'per_proc_s': [round(t, 3) for t in times], 'wall_s': round(wall, 2)}))
+    allc = a.procs or host_cores()
+    v1, n1, b1, w1, hashes = run(1, a.width, a.height, a.bitrate, a.frames, a.mode, a.hash)
+    vn, nn, bn, wn, _ = run(allc, a.width, a.height, a.bitrate, a.frames, a.mode) if allc > 1 else (v1, n1, b1, w1, None)
+    what = {'encdec': 'P frames encoded+decoded', 'enc_i': 'IDR frames encoded', 'dec': 'P frames decoded'}[a.mode]
+    print(json.dumps({'value': vn, 'unit': 'frames/s', 'cores': allc, 'kind': 'port', 'value_1core': v1,
+                      'sample': f'{allc} procs x 1 stream x {a.frames} frames {a.width}x{a.height} at {a.bitrate} bps '
+                                f'({what}; {nn} timed frames, slowest process {bn:.2f} s); 1-core: {n1} frames in {b1:.2f} s',
+                      'wall_s': round(w1 + wn, 2), 'parity_hashes': hashes}))
 
 
 if __name__ == '__main__':

@@ -42,21 +42,34 @@ __global__ void k(uint64_t *out, uint32_t seed, int n) {
         av -= len; if (av < 32) av += 32;
     }
     uint64_t t6 = clock64();
+    int tv[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) tv[j] = (int)(((threadIdx.x + 64 * j) * 2654435761u) & 511);
+    uint32_t q = (uint32_t)av & 511;
+    for (int i = 0; i < n; i++) q = (uint32_t)__builtin_amdgcn_readlane(tv[(q >> 6) & 7], (int)(q & 63)) & 511;
+    uint64_t t7 = clock64();
+    uint32_t q2 = q;
+    for (int i = 0; i < n; i++) {  // select by branch tree on 2 bits x readlane (4 regs)
+        const uint32_t r = q2 >> 6 & 3;
+        int sel = r == 0 ? tv[0] : (r == 1 ? tv[1] : (r == 2 ? tv[2] : tv[3]));
+        q2 = (uint32_t)__builtin_amdgcn_readlane(sel, (int)(q2 & 63)) & 255;
+    }
+    uint64_t t8 = clock64();
     if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = t2 - t1; out[2] = t3 - t2; out[3] = t4 - t3; out[4] = x + y + z + w + bsum + (uint32_t)cache + av;
-                            out[5] = t5 - t4; out[6] = t6 - t5; }
+                            out[5] = t5 - t4; out[6] = t6 - t5; out[7] = t7 - t6; out[8] = t8 - t7; out[9] = q + q2; }
 }
 int main() {
     uint32_t h[4096];
     for (int i = 0; i < 4096; i++) h[i] = (i * 40503u + 17) & 4095;
     hipMemcpyToSymbol(HIP_SYMBOL(c_tab), h, sizeof(h));
-    uint64_t *d; hipMalloc(&d, 64);
-    uint64_t r[7];
+    uint64_t *d; hipMalloc(&d, 128);
+    uint64_t r[10];
     int n = 10000;
     for (int rep = 0; rep < 3; rep++) {
         hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, d, 12345u, n);
-        hipMemcpy(r, d, 56, hipMemcpyDeviceToHost);
-        printf("per iter cycles: 8 SALU chain %.1f | s_load dep %.1f | lds+rfl dep %.1f | readlane dep %.1f | 16 indep SALU %.1f | bitreader step %.1f\n",
-               r[0] / (double)n, r[1] / (double)n, r[2] / (double)n, r[3] / (double)n, r[5] / (double)n, r[6] / (double)n);
+        hipMemcpy(r, d, 80, hipMemcpyDeviceToHost);
+        printf("per iter cycles: 8 SALU chain %.1f | s_load dep %.1f | lds+rfl dep %.1f | readlane dep %.1f | 16 indep SALU %.1f | bitreader step %.1f | vgpr-table(movrel) %.1f | vgpr-table(select4) %.1f\n",
+               r[0] / (double)n, r[1] / (double)n, r[2] / (double)n, r[3] / (double)n, r[5] / (double)n, r[6] / (double)n, r[7] / (double)n, r[8] / (double)n);
     }
     return 0;
 }
