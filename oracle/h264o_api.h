@@ -39,6 +39,11 @@ void h264o_dec_destroy(H264ODec *d);
 int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out_i420, int *w, int *h);
 void h264o_dec_mbinfo(const H264ODec *d, int32_t *out);
 
+/* test-stream helpers (tests/streamgen.py): CAVLC bits of one residual block (0/1 per byte; returns
+ * the bit count, -1 if cap is too small) and the coded_block_pattern codeNum of cbp (Table 9-4) */
+int h264o_cavlc_bits(const int16_t *coef, int maxnum, int nc, uint8_t *bits, int cap);
+int h264o_cbp_code(int cbp, int intra);
+
 /* wrapper colour conversion: rgba_to_yuv (openh264_wrapper.cpp:22-40),
  * yuv_to_rgba_optimized (:150-195) */
 void h264o_rgba_to_i420(const uint8_t *rgba, int w, int h, uint8_t *i420_out);

@@ -497,3 +497,27 @@ void h264o_i420_to_rgba(const uint8_t *y, const uint8_t *u, const uint8_t *v, in
             out[o++] = 255;
         }
 }
+
+/* ---------------- test-stream writing helpers (tests/streamgen.py) ----------------
+ * The CAVLC residual_block writer (9.2, the encoder half's cavlc_write_block) as a bit string of
+ * 0/1 bytes, and the coded_block_pattern code (Table 9-4 inverse), so that the hand-built decoder
+ * test streams share their VLC tables with the oracle rather than restating them a second time. */
+int h264o_cavlc_bits(const int16_t *coef, int maxnum, int nc, uint8_t *bits, int cap) {
+    BW b; bw_init(&b);
+    int tc = 0;
+    cavlc_write_block(&b, coef, maxnum, nc, &tc);
+    int n = (int)(b.len * 8) + b.nacc;
+    if (n > cap) { bw_free(&b); return -1; }
+    for (int i = 0; i < n; i++) {
+        int byte = i >> 3;
+        bits[i] = byte < (int)b.len ? (uint8_t)((b.buf[byte] >> (7 - (i & 7))) & 1)
+                                    : (uint8_t)((b.acc >> (b.nacc - 1 - (i - (int)b.len * 8))) & 1);
+    }
+    bw_free(&b);
+    return n;
+}
+int h264o_cbp_code(int cbp, int intra) {
+    const uint8_t *t = intra ? CBP_INTRA_FROM_CODE : CBP_INTER_FROM_CODE;
+    for (int c = 0; c < 48; c++) if (t[c] == cbp) return c;
+    return -1;
+}

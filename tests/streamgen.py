@@ -77,3 +77,329 @@ def p_frame(mbw, mbh, frame_num, poc_lsb, rng, max_mvd=96, skip_prob=0.2, qp_del
     if run:
         w.ue(run)
     return nal(2, 1, w.rbsp())
+
+
+# ---------------------------------------------------------------------------------------------
+# Full Baseline syntax generator: random but conforming access units that exercise every branch of
+# the decoders' macroblock layer (7.3.5): P_L0_16x16 / 16x8 / 8x16, P_8x8 with every sub_mb_type,
+# P_Skip runs, I_NxN, I_16x16 (all 24 types), I_PCM, mb_qp_delta over its whole range (including the
+# wrap across 0 / 51), coded residuals of every block class with large levels (level_prefix 14 / 15
+# escapes) at low QP, num_ref_idx_active_override, a ref_pic_list_modification that resolves to the
+# single reference, non-zero chroma_qp_index_offset and deblocking filter offsets. Residual blocks are
+# written by the oracle's CAVLC writer (h264o_cavlc_bits); everything else here, from 7.3 syntax.
+# Intra prediction modes are drawn only among the modes whose neighbours are available (8.3.1.2,
+# 8.3.3, 8.3.4), and levels are bounded by QP so that no dequantised value leaves the 16-bit range
+# a conforming stream keeps (8.5.12).
+
+class FastBits:
+    def __init__(self):
+        self.b = bytearray()
+
+    def u(self, v, n):
+        for i in range(n - 1, -1, -1):
+            self.b.append((v >> i) & 1)
+
+    def ue(self, v):
+        k = v + 1
+        n = k.bit_length()
+        self.u(0, n - 1)
+        self.u(k, n)
+
+    def se(self, v):
+        self.ue(2 * v - 1 if v > 0 else -2 * v)
+
+    def align_zero(self):
+        while len(self.b) % 8:
+            self.b.append(0)
+
+    def raw(self, bits):
+        self.b += bits
+
+    def rbsp(self):
+        bits = np.frombuffer(bytes(self.b) + b'\x01', np.uint8)
+        pad = (-len(bits)) % 8
+        bits = np.concatenate([bits, np.zeros(pad, np.uint8)])
+        return np.packbits(bits).tobytes()
+
+
+_I4_NEEDS = {0: 'T', 1: 'L', 2: '', 3: 'T', 4: 'TL', 5: 'TL', 6: 'TL', 7: 'T', 8: 'L'}   # 8.3.1.2.x
+_I16_NEEDS = {0: 'T', 1: 'L', 2: '', 3: 'TL'}                                               # 8.3.3.x
+_CHROMA_NEEDS = {0: '', 1: 'L', 2: 'T', 3: 'TL'}                                            # 8.3.4.x
+_BLK_ORDER = [0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15]  # decoding order -> raster 4x4
+
+
+def _ok(needs, top, left):
+    return ('T' not in needs or top) and ('L' not in needs or left)
+
+
+class SyntaxGen:
+    def __init__(self, oracle_so, mbw, mbh, seed, crop_right=0, crop_bottom=0, cqp=0, init_qp=26):
+        import ctypes
+        self.ct = ctypes
+        L = ctypes.CDLL(oracle_so)
+        L.h264o_cavlc_bits.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.h264o_cbp_code.argtypes = [ctypes.c_int, ctypes.c_int]
+        self.L = L
+        self.mbw, self.mbh = mbw, mbh
+        self.rng = np.random.default_rng(seed)
+        self.crop = (crop_right, crop_bottom)
+        self.cqp, self.init_qp = cqp, init_qp
+        self.frame_num = 0
+        self.poc = 0
+        self.idr_id = 0
+        self._bits = np.zeros(512, np.uint8)
+
+    # ---- parameter sets (7.3.2.1, 7.3.2.2)
+    def sps(self):
+        w = FastBits()
+        w.u(66, 8); w.u(0xC0, 8); w.u(40, 8); w.ue(0)
+        w.ue(12)              # log2_max_frame_num_minus4 (16 bits)
+        w.ue(0); w.ue(12)     # POC type 0, 16-bit lsb
+        w.ue(1); w.u(0, 1)
+        w.ue(self.mbw - 1); w.ue(self.mbh - 1)
+        w.u(1, 1); w.u(1, 1)
+        cr, cb = self.crop
+        w.u(1 if (cr or cb) else 0, 1)
+        if cr or cb:
+            w.ue(0); w.ue(cr); w.ue(0); w.ue(cb)
+        w.u(0, 1)
+        return nal(3, 7, w.rbsp())
+
+    def pps(self):
+        w = FastBits()
+        w.ue(0); w.ue(0); w.u(0, 1); w.u(0, 1); w.ue(0)
+        w.ue(0); w.ue(0)      # num_ref_idx_l0/l1_default_active_minus1
+        w.u(0, 1); w.u(0, 2)
+        w.se(self.init_qp - 26); w.se(0); w.se(self.cqp)
+        w.u(1, 1); w.u(0, 1); w.u(0, 1)
+        return nal(3, 8, w.rbsp())
+
+    # ---- helpers
+    def _nc(self, nn, avail_mb, mx, my, cur, ras):
+        bx, by = ras & 3, ras >> 2
+        na = cur[ras - 1] if bx > 0 else (nn[my][mx - 1][ras + 3] if mx > 0 else None)
+        nb = cur[ras - 4] if by > 0 else (nn[my - 1][mx][ras + 12] if my > 0 else None)
+        return self._avg(na, nb)
+
+    def _ncc(self, nn, mx, my, cur, pl, blk):
+        base = 16 + 4 * pl
+        bx, by = blk & 1, blk >> 1
+        na = cur[base + blk - 1] if bx > 0 else (nn[my][mx - 1][base + blk + 1] if mx > 0 else None)
+        nb = cur[base + blk - 2] if by > 0 else (nn[my - 1][mx][base + blk + 2] if my > 0 else None)
+        return self._avg(na, nb)
+
+    @staticmethod
+    def _avg(na, nb):
+        if na is not None and nb is not None:
+            return (na + nb + 1) >> 1
+        return na if na is not None else (nb if nb is not None else 0)
+
+    def _levels(self, maxnum, qp, big_ok=True):
+        """coefficients in scan order (maxnum of them) for one block, bounded by QP"""
+        rng = self.rng
+        lim = max(1, 2048 // (25 << (qp // 6)))
+        tc = int(rng.choice([0, 1, 1, 2, 3, 4, 6, 8, maxnum // 2, maxnum]))
+        tc = min(tc, maxnum)
+        c = np.zeros(maxnum, np.int16)
+        if tc:
+            pos = rng.choice(maxnum, tc, replace=False)
+            mag = rng.choice([1, 1, 1, 2, 3, 5], tc)
+            if big_ok and lim > 8 and rng.random() < 0.3:
+                mag[int(rng.integers(tc))] = int(rng.integers(8, lim + 1))   # escape codes (level_prefix 14/15)
+            mag = np.minimum(mag, lim)
+            c[pos] = mag * rng.choice([-1, 1], tc)
+        return c
+
+    def _block(self, w, coef, nc):
+        n = self.L.h264o_cavlc_bits(coef.ctypes.data, len(coef), nc, self._bits.ctypes.data, self._bits.size)
+        assert n > 0
+        w.raw(self._bits[:n].tobytes())
+        return int(np.count_nonzero(coef))
+
+    def _residual(self, w, nn, mx, my, cur, mtype, cbp, qp, i16):
+        qpc = _CHROMA_QP[min(51, max(0, qp + self.cqp))]
+        if i16:
+            self._block(w, self._levels(16, qp - 6 if qp >= 6 else 0, big_ok=False), self._nc(nn, None, mx, my, cur, 0))
+        for k in range(16):
+            ras = _BLK_ORDER[k]
+            if not (cbp >> (k >> 2)) & 1:
+                continue
+            coef = self._levels(15 if i16 else 16, qp)
+            cur[ras] = self._block(w, coef, self._nc(nn, None, mx, my, cur, ras))
+        cbpc = cbp >> 4
+        if cbpc:
+            for pl in range(2):
+                self._block(w, self._levels(4, qpc + 6 if qpc + 6 <= 51 else 51, big_ok=False), -1)
+            if cbpc == 2:
+                for pl in range(2):
+                    for blk in range(4):
+                        cur[16 + 4 * pl + blk] = self._block(w, self._levels(15, qpc), self._ncc(nn, mx, my, cur, pl, blk))
+
+    def _qp_delta(self, w, qp):
+        rng = self.rng
+        r = rng.random()
+        if r < 0.5:
+            dq = 0
+        elif r < 0.8:
+            dq = int(rng.integers(-4, 5))
+        else:
+            dq = int(rng.integers(-26, 26))   # wraps across 0 / 51
+        w.se(dq)
+        return (qp + dq + 52) % 52
+
+    def _intra(self, w, nn, i4m, kinds, mx, my, qp, in_p, kind):
+        """I_NxN / I_16x16 / I_PCM macroblock (mb_type already chosen); returns (qp, nnz row, i4 modes)"""
+        rng = self.rng
+        cur = [0] * 24
+        top_mb, left_mb = my > 0, mx > 0
+        off = 5 if in_p else 0
+        modes = None
+        self._last_cbp = 0
+        if kind == 'pcm':
+            w.ue(off + 25)
+            w.align_zero()
+            for _ in range(384):
+                w.u(int(rng.integers(1, 256)), 8)
+            return qp, [16] * 24, None
+        cm = int(rng.choice([m for m, nd in _CHROMA_NEEDS.items() if _ok(nd, top_mb, left_mb)]))
+        if kind == 'i4':
+            w.ue(off + 0)
+            modes = [2] * 16
+            for k in range(16):
+                ras = _BLK_ORDER[k]
+                bx, by = ras & 3, ras >> 2
+                top = by > 0 or top_mb
+                left = bx > 0 or left_mb
+                # predIntra4x4PredMode (8.3.1.1)
+                if (bx == 0 and not left_mb) or (by == 0 and not top_mb):
+                    pm = 2
+                else:
+                    a = modes[ras - 1] if bx > 0 else (i4m[my][mx - 1][ras + 3] if kinds[my][mx - 1] == 'i4' else 2)
+                    b = modes[ras - 4] if by > 0 else (i4m[my - 1][mx][ras + 12] if kinds[my - 1][mx] == 'i4' else 2)
+                    pm = min(a, b)
+                m = int(rng.choice([m for m, nd in _I4_NEEDS.items() if _ok(nd, top, left)]))
+                if rng.random() < 0.3 and _ok(_I4_NEEDS[pm], top, left):
+                    m = pm
+                modes[ras] = m
+                if m == pm:
+                    w.u(1, 1)
+                else:
+                    w.u(0, 1)
+                    w.u(m if m < pm else m - 1, 3)
+            w.ue(cm)
+            cbp = int(rng.integers(0, 48))
+            self._last_cbp = cbp
+            w.ue(self.L.h264o_cbp_code(cbp, 1))
+            if cbp:
+                qp = self._qp_delta(w, qp)
+                self._residual(w, nn, mx, my, cur, 'i4', cbp, qp, False)
+            return qp, cur, modes
+        # I_16x16
+        pm16 = int(rng.choice([m for m, nd in _I16_NEEDS.items() if _ok(nd, top_mb, left_mb)]))
+        cbpc = int(rng.integers(0, 3))
+        cbpl = 15 if rng.random() < 0.5 else 0
+        self._last_cbp = cbpl | (cbpc << 4)
+        w.ue(off + 1 + pm16 + 4 * cbpc + (12 if cbpl else 0))
+        w.ue(cm)
+        qp = self._qp_delta(w, qp)
+        self._residual(w, nn, mx, my, cur, 'i16', cbpl | (cbpc << 4), qp, True)
+        return qp, cur, None
+
+    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24):
+        rng = self.rng
+        mbw, mbh = self.mbw, self.mbh
+        w = FastBits()
+        w.ue(0)
+        w.ue(7 if idr else 5)
+        w.ue(0)
+        w.u(self.frame_num & 0xffff, 16)
+        if idr:
+            w.ue(self.idr_id)
+        w.u(self.poc & 0xffff, 16)
+        if not idr:
+            w.u(1 if override else 0, 1)
+            if override:
+                w.ue(0)                       # num_ref_idx_l0_active_minus1
+            w.u(1 if reorder else 0, 1)       # ref_pic_list_modification_flag_l0
+            if reorder:
+                w.ue(0); w.ue(0)              # subtract 1: picNum of the previous (only) reference
+                w.ue(3)
+        if idr:
+            w.u(0, 1); w.u(0, 1)
+        else:
+            w.u(0, 1)
+        qp_delta = min(51 - self.init_qp, max(-self.init_qp, qp_delta))  # SliceQPY in 0..51
+        qp = self.init_qp + qp_delta
+        w.se(qp_delta)
+        idc, fa, fb = dbk
+        w.ue(idc)
+        if idc != 1:
+            w.se(fa); w.se(fb)
+        nn = [[None] * mbw for _ in range(mbh)]
+        i4m = [[None] * mbw for _ in range(mbh)]
+        kinds = [[None] * mbw for _ in range(mbh)]
+        names = list(mix)
+        probs = np.array([mix[k] for k in names], float)
+        probs /= probs.sum()
+        run = 0
+        self.log = []   # per MB: (mb type code as h264o_dec_mbinfo reports it, QPY, coded_block_pattern)
+        for my in range(mbh):
+            for mx in range(mbw):
+                kind = names[int(rng.choice(len(names), p=probs))]
+                if idr and kind in ('skip', 'p16', 'p16x8', 'p8x16', 'p8x8'):
+                    kind = 'i4'
+                if kind == 'skip':
+                    run += 1
+                    nn[my][mx], kinds[my][mx] = [0] * 24, 'skip'
+                    self.log.append((3, qp, 0))
+                    continue
+                if not idr:
+                    w.ue(run)
+                    run = 0
+                kinds[my][mx] = kind
+                if kind in ('i4', 'i16', 'pcm'):
+                    qp, nn[my][mx], i4m[my][mx] = self._intra(w, nn, i4m, kinds, mx, my, qp, not idr, kind)
+                    self.log.append(({'i4': 0, 'i16': 1, 'pcm': 7}[kind], qp, self._last_cbp))
+                    continue
+                cur = [0] * 24
+                mt = {'p16': 0, 'p16x8': 1, 'p8x16': 2, 'p8x8': 3}[kind]
+                w.ue(mt)
+                if mt < 3:
+                    for _ in range(1 if mt == 0 else 2):
+                        w.se(int(rng.integers(-max_mvd, max_mvd + 1))); w.se(int(rng.integers(-max_mvd, max_mvd + 1)))
+                else:
+                    subs = [int(rng.integers(0, 4)) for _ in range(4)]
+                    for s in subs:
+                        w.ue(s)
+                    for s in subs:
+                        for _ in range({0: 1, 1: 2, 2: 2, 3: 4}[s]):
+                            w.se(int(rng.integers(-max_mvd, max_mvd + 1))); w.se(int(rng.integers(-max_mvd, max_mvd + 1)))
+                cbp = int(rng.integers(0, 48)) if rng.random() < 0.85 else 0
+                w.ue(self.L.h264o_cbp_code(cbp, 0))
+                if cbp:
+                    qp = self._qp_delta(w, qp)
+                    self._residual(w, nn, mx, my, cur, kind, cbp, qp, False)
+                nn[my][mx] = cur
+                self.log.append(({'p16': 2, 'p16x8': 4, 'p8x16': 5, 'p8x8': 6}[kind], qp, cbp))
+        if run:
+            w.ue(run)
+        return w.rbsp()
+
+    def idr(self, mix=None, **kw):
+        """SPS + PPS + IDR picture (I_NxN / I_16x16 / I_PCM)"""
+        self.frame_num, self.poc = 0, 0
+        body = self._slice(True, mix or {'i4': 5, 'i16': 4, 'pcm': 1}, **kw)
+        self.idr_id = (self.idr_id + 1) & 0xffff
+        self.frame_num, self.poc = 1, 2
+        return self.sps() + self.pps() + nal(3, 5, body)
+
+    def p(self, mix=None, **kw):
+        """one P picture with every macroblock type"""
+        mix = mix or {'skip': 3, 'p16': 3, 'p16x8': 2, 'p8x16': 2, 'p8x8': 3, 'i4': 1, 'i16': 1, 'pcm': 0.3}
+        body = self._slice(False, mix, **kw)
+        self.frame_num = (self.frame_num + 1) & 0xffff
+        self.poc += 2
+        return nal(2, 1, body)
+
+
+_CHROMA_QP = [i for i in range(30)] + [29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39]

@@ -1,0 +1,55 @@
+"""CPU: the full-syntax test-stream generator (tests/streamgen.py SyntaxGen) against the oracle
+decoder. Every macroblock the generator writes -- P_L0_16x16 / 16x8 / 8x16, P_8x8 with all four
+sub_mb_types, P_Skip runs, I_NxN, I_16x16, I_PCM, mb_qp_delta across its whole range -- is parsed by
+the oracle with the same type, QPY and coded_block_pattern (h264o_dec_mbinfo), under cropping,
+non-zero chroma_qp_index_offset, deblocking offsets / idc 2, num_ref_idx_active_override and a
+ref_pic_list_modification. These streams are what tests/test_gpu_syntax.py decodes on the GPU."""
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, 'oracle', 'build', 'libh264_oracle.so')
+
+CASES = [  # (mbw, mbh, crop_right, crop_bottom, chroma_qp_index_offset, pic_init_qp, seed)
+    (11, 9, 0, 0, 0, 26, 1),
+    (11, 9, 4, 2, -7, 20, 2),
+    (11, 9, 0, 0, 12, 34, 3),
+    (5, 3, 2, 0, -12, 8, 4),
+]
+SLICES = [dict(), dict(qp_delta=4, dbk=(0, 3, -2), override=True), dict(qp_delta=-9, dbk=(2, -6, 6), reorder=True),
+          dict(dbk=(1, 0, 0), override=True, reorder=True)]
+
+
+def _stream(oracle, case):
+    from streamgen import SyntaxGen
+    mbw, mbh, cr, cb, cqp, iqp, seed = case
+    g = SyntaxGen(SO, mbw, mbh, seed, crop_right=cr, crop_bottom=cb, cqp=cqp, init_qp=iqp)
+    units, logs = [g.idr()], []
+    logs.append(g.log)
+    for kw in SLICES:
+        units.append(g.p(**kw))
+        logs.append(g.log)
+    return units, logs
+
+
+@pytest.mark.parametrize('case', CASES, ids=[f'{c[0]}x{c[1]}_crop{c[2]}{c[3]}_cqp{c[4]}' for c in CASES])
+def test_oracle_parses_every_generated_macroblock(oracle, case):
+    units, logs = _stream(oracle, case)
+    d = oracle.decoder()
+    mbw, mbh = case[0], case[1]
+    seen_types, wraps = set(), 0
+    for k, (u, log) in enumerate(zip(units, logs)):
+        rc, pic, w, h = d.decode(u)
+        assert rc == 1, f'unit {k}'
+        assert (w, h) == (mbw * 16 - 2 * case[2], mbh * 16 - 2 * case[3])
+        mi = np.zeros(mbw * mbh * 8, np.int32)
+        oracle.L.h264o_dec_mbinfo(d.d, mi.ctypes.data)
+        got = [tuple(int(x) for x in r[:3]) for r in mi.reshape(-1, 8)]
+        assert got == log, f'unit {k}: first mismatch at MB {next(i for i, (a, b) in enumerate(zip(got, log)) if a != b)}'
+        seen_types |= {t for t, _, _ in log}
+        wraps += sum(1 for a, b in zip(log, log[1:]) if abs(a[1] - b[1]) > 26)
+    if mbw * mbh >= 99:
+        assert seen_types == {0, 1, 2, 3, 4, 5, 6, 7}, seen_types   # every mb type class
+        assert wraps > 0                                             # QP wrapped across 0 / 51
