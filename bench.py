@@ -98,6 +98,7 @@ def gpu_parity(a, oracle_hashes, i_only=False):
         return False, 'no oracle hashes (CPU baseline leg failed or skipped)'
     g = SyntheticStream(0, a.width, a.height)
     enc = h264mi.BatchEncoder(a.width, a.height, a.bitrate, 1)
+    enc.set_frame_skip(False)  # as the timed encoder (see bench_encode)
     dec = h264mi.BatchDecoder(a.width, a.height, 1)
     ok = True
     for t, want in enumerate(oracle_hashes):
@@ -234,6 +235,9 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # overlaps the entropy decoding of g and the reconstruction of g-1.
     es, ds = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
     enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
+    # frame skipping off: every step codes a frame (at 1 Mbps the synthetic 1080p content overflows
+    # the rate control's buffer and most frames would be dropped)
+    enc.set_frame_skip(False)
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G) if decode else None
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
@@ -312,7 +316,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     cfg = {'workload': f'{W}x{H} {work}, {S} streams per GPU, {a.bitrate} bps, wrapper encoder params'
                        + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
            'baseline_config': {0: 'metric (configs[2] x 8 streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
-           'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'parallelism': f'streams x{world} (weak)'}
+           'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
+           'parallelism': f'streams x{world} (weak)'}
     return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg,
             'roofline': roofline('enc_mb_kernel', alg, ems, en, a), 'kernels': kern,
             'selfcheck_ok': selfcheck_ok,
@@ -329,6 +334,7 @@ def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
     F = W * H * 3 // 2
     g = SyntheticStream(0, W, H)
     enc = h264mi.BatchEncoder(W, H, a.bitrate, 1)
+    enc.set_frame_skip(False)  # a.clip coded frames
     slot = 1 << 21
     n = a.clip
     units = torch.empty((n, slot), dtype=torch.uint8, device=dev)

@@ -83,6 +83,9 @@ h264mi_encoder *h264mi_enc_create(int width, int height, int bitrate, int nstrea
 void h264mi_enc_destroy(h264mi_encoder *e);
 int h264mi_enc_force_idr(h264mi_encoder *e, int stream);            /* stream < 0: all */
 int h264mi_enc_encode(h264mi_encoder *e, const void *d_frames);     /* async; nstreams tight I420 frames back to back */
+/* rate-control frame skipping (on by default, as the wrapper's OpenH264): a skipped frame has 0 NAL bytes */
+int h264mi_enc_set_frame_skip(h264mi_encoder *e, int enable);
+int h264mi_enc_frames_skipped(h264mi_encoder *e, int stream);
 int h264mi_enc_sync(h264mi_encoder *e);
 int h264mi_enc_nal_bytes(h264mi_encoder *e, int *out_bytes);        /* sync; -2 if a kernel reported an error */
 const void *h264mi_enc_nal_ptr(h264mi_encoder *e, int stream);     /* Annex-B bytes of the last frame (device) */

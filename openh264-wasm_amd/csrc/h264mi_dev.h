@@ -296,4 +296,15 @@ template <class P> DEV bool gran_poll(P g, bool need, uint32_t epoch, uint64_t &
     }
 }
 
+// QPY entering MB row r of an encoder frame: the slice QP for row 0, else the value
+// row r - 1 publishes in rowq[r] (its row QP as soon as it codes an MB carrying mb_qp_delta, or the
+// QPY it entered with if it codes none). Wave-uniform; false on abort/timeout.
+template <class P> DEV bool row_entry_qp(P rowq, int r, int slice_qp, uint32_t epoch, int32_t *abort_word, int *qp) {
+    if (r == 0) { *qp = slice_qp; return true; }
+    uint32_t v = 0;
+    if (!gran_wait(rowq + r, 1, epoch, &v, abort_word)) return false;
+    *qp = __builtin_amdgcn_readfirstlane((int)v);
+    return true;
+}
+
 }  // namespace h264mi

@@ -61,6 +61,11 @@ struct EncState {
     int32_t nal_bytes;     // bytes of the last coded frame (all NAL units, start codes included)
     int32_t err;           // nonzero: a kernel detected an error / timeout
     int64_t last_bits;
+    int64_t vbuf;          // rate control: virtual buffer fullness in bits
+    int32_t cur_skip;      // 1 if the frame being coded is skipped by the rate control (0 bytes out)
+    int32_t skip_en;       // frame skipping enabled (the wrapper's default)
+    int32_t skipped;       // frames skipped so far
+    int32_t pad_s;
     int32_t sps_bytes, pps_bytes;
     uint8_t sps[64], pps[32];
 };
@@ -88,6 +93,9 @@ struct EncDesc {
     int32_t ps, psc;        // row strides of pl / plc
     int32_t pad3[2];
     uint64_t *egran;        // MB -> deblocking hand-off, 128 granules per MB (deblock.inc DbkSrcGranules)
+    int32_t *rowqp;         // MB-row (GOM) QP plan of the frame being coded (written by the previous pack)
+    int32_t *rowbits;       // macroblock_layer() bits per MB row of the last coded frame
+    uint64_t *rowq;         // per MB row: {epoch, QPY entering the row} granules (row r publishes r + 1)
 };
 
 // One stream's padded reference planes and the picture they are built from (enc_planes.inc).

@@ -42,6 +42,8 @@ def lib():
             'h264mi_enc_destroy': (None, [vp]),
             'h264mi_enc_force_idr': (i, [vp, i]),
             'h264mi_enc_encode': (i, [vp, vp]),
+            'h264mi_enc_set_frame_skip': (i, [vp, i]),
+            'h264mi_enc_frames_skipped': (i, [vp, i]),
             'h264mi_enc_sync': (i, [vp]),
             'h264mi_enc_nal_bytes': (i, [vp, vp]),
             'h264mi_enc_nal_ptr': (vp, [vp, i]),
@@ -206,6 +208,14 @@ class BatchEncoder:
 
     def force_idr(self, stream=-1):
         self._L.h264mi_enc_force_idr(self._e, stream)
+
+    def set_frame_skip(self, on):
+        """rate-control frame skipping (on by default, as the wrapper's encoder)"""
+        if self._L.h264mi_enc_set_frame_skip(self._e, 1 if on else 0) != 0:
+            raise RuntimeError('h264mi_enc_set_frame_skip failed')
+
+    def frames_skipped(self, s=0):
+        return self._L.h264mi_enc_frames_skipped(self._e, s)
 
     def nal_sizes(self):
         out = (ctypes.c_int * self.S)()

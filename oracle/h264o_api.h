@@ -26,6 +26,11 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *i420, uint8_t *out, int cap); /
 void h264o_enc_recon(const H264OEnc *e, uint8_t *i420_out);   /* deblocked recon, tight I420 */
 void h264o_enc_mbinfo(const H264OEnc *e, int32_t *out);       /* 8 x int32 per MB */
 int h264o_enc_last_qp(const H264OEnc *e);
+/* frame skipping is on by default, as in the wrapper's OpenH264 configuration;
+ * a skipped frame encodes to 0 bytes */
+void h264o_enc_set_frame_skip(H264OEnc *e, int enable);
+int h264o_enc_frames_skipped(const H264OEnc *e);
+int h264o_rc_row_delta(int64_t row_bits, int64_t mean);
 int h264o_rc_init_qp(int w, int h, int bitrate);
 int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr);
 size_t h264o_write_sps(int w, int h, uint8_t *out);

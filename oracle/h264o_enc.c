@@ -22,6 +22,7 @@
 #define QP_MAX 51
 #define LOG2_MAX_FRAME_NUM 16
 #define LOG2_MAX_POC_LSB 16
+#define CROSS_THR 1024  /* cross search when the best integer cost exceeds this */
 
 struct H264OEnc {
     int w, h, mbw, mbh, cw, ch;
@@ -33,6 +34,11 @@ struct H264OEnc {
     int qp;
     int last_qp, last_idr;
     int64_t last_bits;
+    /* GOM (MB-row) rate control and frame skipping */
+    int *rowqp;       /* QP plan of the next frame, one per MB row */
+    int64_t *rowbits; /* macroblock_layer() bits per MB row of the last coded frame */
+    int64_t vbuf;     /* virtual buffer fullness (bits) */
+    int skip_en, skipped;
 };
 
 /* ---------------- rate control ---------------- */
@@ -59,6 +65,23 @@ int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr) {
     else d = 0;
     return clip3(QP_MIN, QP_MAX, qp + d);
 }
+/* MB-row ("GOM") QP plan of the next frame around its frame QP: rows that cost more than the mean
+ * in the last coded frame are quantised more coarsely, cheaper rows more finely. */
+int h264o_rc_row_delta(int64_t row_bits, int64_t mean) {
+    if (mean <= 0) return 0;
+    if (row_bits > 2 * mean) return 2;
+    if (4 * row_bits > 5 * mean) return 1;
+    if (2 * row_bits < mean) return -1;
+    return 0;
+}
+static void rc_plan_rows(H264OEnc *e) {
+    int64_t sum = 0;
+    for (int r = 0; r < e->mbh; r++) sum += e->rowbits[r];
+    int64_t mean = sum / e->mbh;
+    for (int r = 0; r < e->mbh; r++) e->rowqp[r] = clip3(QP_MIN, QP_MAX, e->qp + h264o_rc_row_delta(e->rowbits[r], mean));
+}
+/* mb_qp_delta carrying QP a from QP_pred b, wrapped into -26..25 (7.4.5) */
+static int qp_delta_wrap(int a, int b) { return ((a - b + 26 + 52) % 52) - 26; }
 static int level_idc_for(int mbs) {
     static const int L[][3] = {{10, 99, 1485},    {11, 396, 3000},    {12, 396, 6000},     {13, 396, 11880},
                                {20, 396, 11880},  {21, 792, 19800},   {22, 1620, 20250},   {30, 1620, 40500},
@@ -408,12 +431,27 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
         /* chroma already reconstructed with zero residual == prediction */
         return;
     }
-    /* 2. integer ME: candidates, then iterated small diamond */
-    /* integer search range: +-16 pel around (0,0) (DESIGN.md §3.5) */
+    /* 2. integer ME: start candidates {mvp, (0,0), A, B, C} (the MV predictors'
+     * neighbours, integer-rounded), iterated small diamond, then -- when the match is still poor --
+     * a cross search along the full horizontal and vertical lines through the best point */
+    /* integer search range: +-16 pel around (0,0) */
     const int xmin = -16, xmax = 16, ymin = -16, ymax = 16;
-    int cand[2][2] = {{(mvp[0] + 2) >> 2, (mvp[1] + 2) >> 2}, {0, 0}};
+    int cand[5][2], ncand = 0;
+    cand[ncand][0] = (mvp[0] + 2) >> 2; cand[ncand][1] = (mvp[1] + 2) >> 2; ncand++;
+    cand[ncand][0] = 0; cand[ncand][1] = 0; ncand++;
+    {
+        const MBInfo *nb[3] = {mbx > 0 ? &e->mbs[mby * e->mbw + mbx - 1] : NULL, mby > 0 ? &e->mbs[(mby - 1) * e->mbw + mbx] : NULL,
+                               mby > 0 ? (mbx + 1 < e->mbw ? &e->mbs[(mby - 1) * e->mbw + mbx + 1]
+                                                           : (mbx > 0 ? &e->mbs[(mby - 1) * e->mbw + mbx - 1] : NULL)) : NULL};
+        for (int i = 0; i < 3; i++) {
+            const MBInfo *m = nb[i];
+            if (m && !mb_is_intra(m->type)) {
+                cand[ncand][0] = (m->mv[0][0] + 2) >> 2; cand[ncand][1] = (m->mv[0][1] + 2) >> 2; ncand++;
+            }
+        }
+    }
     int bx = 0, by = 0, bc = -1;
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < ncand; i++) {
         int cx = clip3(xmin, xmax, cand[i][0]), cy = clip3(ymin, ymax, cand[i][1]);
         int c = sad16_int(e, mbx, mby, cx, cy) + lam * mvbits(4 * cx, 4 * cy, mvp);
         if (bc < 0 || c < bc) { bc = c; bx = cx; by = cy; }
@@ -428,6 +466,15 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
             if (nb < 0 || c < nb) { nb = c; nx = cx; ny = cy; }
         }
         if (nb >= 0 && nb < bc) { bc = nb; bx = nx; by = ny; } else break;
+    }
+    if (bc > CROSS_THR) {  /* horizontal line (x ascending), then vertical line (y ascending) */
+        int cbx = bx, cby = by, cbc = bc;
+        for (int k = 0; k < 66; k++) {
+            int cx = k < 33 ? xmin + k : bx, cy = k < 33 ? by : ymin + (k - 33);
+            int c = sad16_int(e, mbx, mby, cx, cy) + lam * mvbits(4 * cx, 4 * cy, mvp);
+            if (c < cbc) { cbc = c; cbx = cx; cby = cy; }
+        }
+        bc = cbc; bx = cbx; by = cby;
     }
     /* 3. half then quarter refinement by SATD */
     static const int SUB[8][2] = {{0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
@@ -504,7 +551,7 @@ static void write_residual(BW *b, H264OEnc *e, MBInfo *mb, int mbx, int mby) {
                     cavlc_write_block(b, mb->cac[pl][blk] + 1, 15, nc_chroma(e->mbs, mb, e->mbw, mbx, mby, pl, blk), &tot);
     }
 }
-static void write_mb(BW *b, H264OEnc *e, MBInfo *mb, int mbx, int mby, int pslice) {
+static void write_mb(BW *b, H264OEnc *e, MBInfo *mb, int mbx, int mby, int pslice, int dqp) {
     int off = pslice ? 5 : 0;
     if (mb->type == MBT_I4) {
         bw_ue(b, off + 0);
@@ -517,17 +564,17 @@ static void write_mb(BW *b, H264OEnc *e, MBInfo *mb, int mbx, int mby, int pslic
         }
         bw_ue(b, mb->cmode);
         bw_ue(b, cbp_code(mb->cbp, 1));
-        if (mb->cbp) bw_se(b, 0);
+        if (mb->cbp) bw_se(b, dqp);
     } else if (mb->type == MBT_I16) {
         bw_ue(b, off + 1 + mb->i16mode + 4 * (mb->cbp >> 4) + 12 * ((mb->cbp & 15) ? 1 : 0));
         bw_ue(b, mb->cmode);
-        bw_se(b, 0);
+        bw_se(b, dqp);
     } else { /* P16x16 */
         bw_ue(b, 0);
         bw_se(b, mb->mvd[0][0]);
         bw_se(b, mb->mvd[0][1]);
         bw_ue(b, cbp_code(mb->cbp, 0));
-        if (mb->cbp) bw_se(b, 0);
+        if (mb->cbp) bw_se(b, dqp);
     }
     write_residual(b, e, mb, mbx, mby);
 }
@@ -544,16 +591,22 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
         e->src[p] = (uint8_t *)calloc(n, 1); e->rec[p] = (uint8_t *)calloc(n, 1); e->ref[p] = (uint8_t *)calloc(n, 1);
     }
     e->mbs = (MBInfo *)calloc((size_t)e->mbw * e->mbh, sizeof(MBInfo));
+    e->rowqp = (int *)calloc((size_t)e->mbh, sizeof(int));
+    e->rowbits = (int64_t *)calloc((size_t)e->mbh, sizeof(int64_t));
     e->first = 1;
+    e->skip_en = 1;  /* the wrapper leaves OpenH264's frame skipping on (bEnableFrameSkip default) */
     e->qp = h264o_rc_init_qp(w, h, bitrate);
+    rc_plan_rows(e);
     e->idr_pic_id = -1;
     return e;
 }
 void h264o_enc_destroy(H264OEnc *e) {
     if (!e) return;
     for (int p = 0; p < 3; p++) { free(e->src[p]); free(e->rec[p]); free(e->ref[p]); }
-    free(e->mbs); free(e);
+    free(e->mbs); free(e->rowqp); free(e->rowbits); free(e);
 }
+void h264o_enc_set_frame_skip(H264OEnc *e, int enable) { if (e) e->skip_en = enable != 0; }
+int h264o_enc_frames_skipped(const H264OEnc *e) { return e ? e->skipped : 0; }
 void h264o_enc_force_idr(H264OEnc *e) { if (e) e->force_idr = 1; }
 int h264o_enc_last_qp(const H264OEnc *e) { return e->last_qp; }
 
@@ -573,8 +626,16 @@ static void load_source(H264OEnc *e, const uint8_t *yuv) {
 
 int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     if (!e || !yuv || !out) return 0;
-    load_source(e, yuv);
     int idr = e->first || e->force_idr;
+    const int64_t T = e->bitrate / RC_FPS;
+    /* frame skip: a non-IDR frame is dropped while the virtual buffer holds more
+     * than half a second of bits; nothing else changes (reference, frame_num, POC, QP plan) */
+    if (!idr && e->skip_en && e->vbuf > e->bitrate / 2) {
+        e->vbuf = e->vbuf > T ? e->vbuf - T : 0;
+        e->skipped++;
+        return 0;
+    }
+    load_source(e, yuv);
     e->first = 0; e->force_idr = 0;
     if (idr) { e->frame_num = 0; e->poc = 0; e->idr_pic_id = (e->idr_pic_id + 1) & 0xffff; }
     int qp = e->qp;
@@ -593,21 +654,32 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     if (idr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } else bw_put(&b, 0, 1);
     bw_se(&b, qp - 26);
     bw_ue(&b, 0); bw_se(&b, 0); bw_se(&b, 0);
-    /* slice_data() */
-    int skip_run = 0;
-    for (int mby = 0; mby < e->mbh; mby++)
+    /* slice_data(): each MB is decided and quantised at its row's QP; an MB that carries
+     * mb_qp_delta (I16, or coded_block_pattern != 0) moves the running QP there; any other MB's
+     * QPY is the running QP (7.4.5) */
+    int skip_run = 0, running = qp;
+    for (int mby = 0; mby < e->mbh; mby++) {
+        const int qrow = e->rowqp[mby];
+        e->rowbits[mby] = 0;
         for (int mbx = 0; mbx < e->mbw; mbx++) {
             MBInfo *mb = &e->mbs[mby * e->mbw + mbx];
             memset(mb, 0, sizeof(*mb));
-            mb->qp = qp;
+            mb->qp = qrow;
             for (int i = 0; i < 16; i++) mb->i4mode[i] = 2;
             for (int i = 0; i < 4; i++) mb->ref[i] = -1;
             if (idr) encode_intra_mb(e, mb, mbx, mby);
             else encode_p_mb(e, mb, mbx, mby);
+            const int carries = mb->type == MBT_I16 || (mb->type != MBT_PSKIP && mb->cbp != 0);
+            const int dqp = carries ? qp_delta_wrap(qrow, running) : 0;
+            if (carries) running = qrow;
+            mb->qp = running;
             if (mb->type == MBT_PSKIP) { skip_run++; continue; }
             if (!idr) { bw_ue(&b, (uint32_t)skip_run); skip_run = 0; }
-            write_mb(&b, e, mb, mbx, mby, !idr);
+            const int64_t b0 = bw_bits(&b);
+            write_mb(&b, e, mb, mbx, mby, !idr, dqp);
+            e->rowbits[mby] += bw_bits(&b) - b0;
         }
+    }
     if (skip_run) bw_ue(&b, (uint32_t)skip_run);
     bw_trailing(&b);
     o += nal_write(tmp + o, 3, idr ? 5 : 1, b.buf, b.len);
@@ -617,7 +689,9 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     for (int p = 0; p < 3; p++) { uint8_t *t = e->ref[p]; e->ref[p] = e->rec[p]; e->rec[p] = t; }
     e->last_qp = qp; e->last_idr = idr;
     e->last_bits = (int64_t)o * 8;
+    e->vbuf = e->vbuf + e->last_bits > T ? e->vbuf + e->last_bits - T : 0;
     e->qp = h264o_rc_next_qp(qp, e->last_bits, e->bitrate, idr);
+    rc_plan_rows(e);
     e->frame_num = (e->frame_num + 1) & ((1 << LOG2_MAX_FRAME_NUM) - 1);
     e->poc += 2;
     int n = (int)o;

@@ -16,6 +16,8 @@ class Oracle:
         L.h264o_enc_recon.argtypes = [vp, vp]
         L.h264o_enc_mbinfo.argtypes = [vp, vp]
         L.h264o_enc_last_qp.argtypes = [vp]
+        L.h264o_enc_set_frame_skip.argtypes = [vp, ctypes.c_int]
+        L.h264o_enc_frames_skipped.argtypes = [vp]
         L.h264o_rc_init_qp.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.h264o_rc_next_qp.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
         L.h264o_write_sps.restype = ctypes.c_size_t
@@ -64,6 +66,9 @@ class OEnc:
 
     def force_idr(self):
         self.L.h264o_enc_force_idr(self.e)
+
+    def set_frame_skip(self, on):
+        self.L.h264o_enc_set_frame_skip(self.e, 1 if on else 0)
 
     def recon(self):
         out = np.zeros(self.w * self.h * 3 // 2, np.uint8)

@@ -63,6 +63,12 @@ def run_case(oracle, name, w, h, br, n, force_every, kind):
         if force_every and t % force_every == 0 and t > 0:
             enc.force_idr()
         nal = enc.encode(f)
+        if not nal:  # frame skipped by rate control: nothing to decode
+            for k in ('nal_sha256', 'dec_sha256', 'recon_sha256'):
+                out[k].append(None)
+            out['nal_sizes'].append(0)
+            out['qp'].append(None)
+            continue
         rc, pic, dw, dh = dec.decode(nal)
         assert rc == 1 and (dw, dh) == (w, h), (name, t, rc)
         recon = enc.recon()

@@ -91,6 +91,7 @@ def test_pipelined_two_stream_decode(gpu_lib, use_event):
     torch.cuda.synchronize()
     es, ds = torch.cuda.Stream(), torch.cuda.Stream()
     enc = h264mi.BatchEncoder(w, h, 2000000, S, stream=es)
+    enc.set_frame_skip(False)
     dec = h264mi.BatchDecoder(w, h, S, stream=ds, max_frames=G)
     slot = 1 << 20
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device='cuda') for _ in range(2)]

@@ -73,6 +73,7 @@ def _oracle_1080p_stream(oracle, nf, br=1000000, sid=0):
     from h264mi.synth import SyntheticStream
     g = SyntheticStream(sid, 1920, 1080)
     oe, od = oracle.encoder(1920, 1080, br), oracle.decoder()
+    oe.set_frame_skip(False)  # every frame coded (at 1 Mbps this content would overflow the RC buffer)
     units, pics = [], []
     for t in range(nf):
         u = oe.encode(np.ascontiguousarray(g.frame(t)))
@@ -122,6 +123,7 @@ def test_config4_ring_fanout_1080p(gpu_lib, oracle):
     es = torch.cuda.Stream()
     dss = [torch.cuda.Stream() for _ in range(D)]
     enc = h264mi.BatchEncoder(1920, 1080, 1000000, 1, stream=es)
+    enc.set_frame_skip(False)
     decs = [h264mi.BatchDecoder(1920, 1080, 1, stream=dss[k]) for k in range(D)]
     ring = h264mi.NalRing(slots=4, slot_bytes=1 << 21)
     for t in range(nf):

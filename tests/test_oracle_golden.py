@@ -1,5 +1,6 @@
 """CPU: the oracle (TEST INFRASTRUCTURE) against the committed fixtures, and its internal
 consistency (decoder output == encoder reconstruction, every frame)."""
+import ctypes
 import hashlib
 import json
 import os
@@ -56,6 +57,41 @@ def test_rc_update_direction(oracle):
     assert L.h264o_rc_next_qp(30, target // 10, br, 0) < 30
     assert L.h264o_rc_next_qp(51, 100 * target, br, 0) == 51
     assert L.h264o_rc_next_qp(12, 0, br, 0) == 12
+
+
+def test_rc_row_plan(oracle):
+    """MB-row (GOM) QP plan: rows costlier than the mean get +1 / +2, cheap rows -1"""
+    f = oracle.L.h264o_rc_row_delta
+    f.argtypes = [ctypes.c_int64, ctypes.c_int64]
+    assert [f(b, 1000) for b in (0, 499, 500, 1000, 1250, 1251, 2000, 2001)] == [-1, -1, 0, 0, 0, 1, 1, 2]
+    assert f(5, 0) == 0
+
+
+def test_frame_skip_and_row_qp_in_stream(oracle):
+    """at a bitrate far below the content's cost, non-IDR frames are skipped (0 bytes) while the
+    virtual buffer holds more than half a second of bits; coded P frames carry mb_qp_delta != 0
+    (per-row QPs) and still decode to the encoder's reconstruction; with skipping off every frame
+    is coded"""
+    from h264mi.synth import SyntheticStream
+    w, h = 352, 288
+    g = SyntheticStream(2, w, h)
+    frames = [np.ascontiguousarray(g.frame(t)) for t in range(10)]
+    oe, od = oracle.encoder(w, h, 60000), oracle.decoder()
+    sizes, qps_seen = [], set()
+    for f in frames:
+        nal = oe.encode(f)
+        sizes.append(len(nal))
+        if nal:
+            rc, pic, _, _ = od.decode(nal)
+            assert rc == 1 and np.array_equal(pic, oe.recon())
+            mi = np.zeros((w // 16) * (h // 16) * 8, np.int32)
+            oracle.L.h264o_dec_mbinfo(od.d, mi.ctypes.data)
+            qps_seen |= set(mi.reshape(-1, 8)[:, 1].tolist())
+    assert sizes[0] > 0 and 0 in sizes and oracle.L.h264o_enc_frames_skipped(oe.e) == sizes.count(0)
+    assert len(qps_seen) > 1, qps_seen   # more than one QPY within pictures: mb_qp_delta was coded
+    oe2 = oracle.encoder(w, h, 60000)
+    oracle.L.h264o_enc_set_frame_skip(oe2.e, 0)
+    assert all(len(oe2.encode(f)) > 0 for f in frames)
 
 
 def test_parameter_sets_are_baseline(oracle):

@@ -16,9 +16,11 @@ def main(w, h, br, S, nf, dev=1, G=1):
     O = ctypes.CDLL(os.path.join(ROOT, 'oracle/build/libh264_oracle.so'))
     O.h264o_enc_create.restype = ctypes.c_void_p
     oe = ctypes.c_void_p(O.h264o_enc_create(w, h, br))
+    O.h264o_enc_set_frame_skip(oe, 0)  # the batch pipeline under test decodes every frame
     F = w * h * 3 // 2
     gens = [SyntheticStream(s, w, h) for s in range(S)]
     enc = h264mi.BatchEncoder(w, h, br, S)
+    enc.set_frame_skip(False)
     dec = h264mi.BatchDecoder(w, h, S, max_frames=G)
     out = np.zeros(w * h * 4, np.uint8)
     slot = 1 << 21

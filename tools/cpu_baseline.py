@@ -29,6 +29,7 @@ def worker(args):
     S = SyntheticStream(stream, w, h)
     frames = [np.ascontiguousarray(S.frame(t)) for t in range(nframes)]
     e = vp(O.h264o_enc_create(w, h, bitrate))
+    O.h264o_enc_set_frame_skip(e, 0)  # as bench.py's GPU encoder: every frame coded
     d = vp(O.h264o_dec_create())
     out = np.zeros(w * h * 4, np.uint8)
     pic = np.zeros(w * h * 3 // 2, np.uint8)
