@@ -30,6 +30,9 @@ int h264o_enc_last_qp(const H264OEnc *e);
  * a skipped frame encodes to 0 bytes */
 void h264o_enc_set_frame_skip(H264OEnc *e, int enable);
 int h264o_enc_frames_skipped(const H264OEnc *e);
+/* motion-search stage counters since creation: cross searches run, cross searches that moved the
+ * vector, start points won by a neighbour candidate (A, B or C) */
+void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]);
 int h264o_rc_row_delta(int64_t row_bits, int64_t mean);
 int h264o_rc_init_qp(int w, int h, int bitrate);
 int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr);

@@ -39,6 +39,7 @@ struct H264OEnc {
     int64_t *rowbits; /* macroblock_layer() bits per MB row of the last coded frame */
     int64_t vbuf;     /* virtual buffer fullness (bits) */
     int skip_en, skipped;
+    int stat_cross, stat_cross_moved, stat_nb_start;  /* ME path counters (tests: coverage of the search stages) */
 };
 
 /* ---------------- rate control ---------------- */
@@ -454,7 +455,7 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
     for (int i = 0; i < ncand; i++) {
         int cx = clip3(xmin, xmax, cand[i][0]), cy = clip3(ymin, ymax, cand[i][1]);
         int c = sad16_int(e, mbx, mby, cx, cy) + lam * mvbits(4 * cx, 4 * cy, mvp);
-        if (bc < 0 || c < bc) { bc = c; bx = cx; by = cy; }
+        if (bc < 0 || c < bc) { bc = c; bx = cx; by = cy; if (i >= 2) e->stat_nb_start++; }
     }
     static const int DIA[4][2] = {{0, -1}, {-1, 0}, {1, 0}, {0, 1}};
     for (int it = 0; it < 32; it++) {
@@ -474,6 +475,8 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
             int c = sad16_int(e, mbx, mby, cx, cy) + lam * mvbits(4 * cx, 4 * cy, mvp);
             if (c < cbc) { cbc = c; cbx = cx; cby = cy; }
         }
+        e->stat_cross++;
+        if (cbx != bx || cby != by) e->stat_cross_moved++;
         bc = cbc; bx = cbx; by = cby;
     }
     /* 3. half then quarter refinement by SATD */
@@ -607,6 +610,9 @@ void h264o_enc_destroy(H264OEnc *e) {
 }
 void h264o_enc_set_frame_skip(H264OEnc *e, int enable) { if (e) e->skip_en = enable != 0; }
 int h264o_enc_frames_skipped(const H264OEnc *e) { return e ? e->skipped : 0; }
+void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]) {
+    out[0] = e->stat_cross; out[1] = e->stat_cross_moved; out[2] = e->stat_nb_start;
+}
 void h264o_enc_force_idr(H264OEnc *e) { if (e) e->force_idr = 1; }
 int h264o_enc_last_qp(const H264OEnc *e) { return e->last_qp; }
 

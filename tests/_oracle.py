@@ -18,6 +18,7 @@ class Oracle:
         L.h264o_enc_last_qp.argtypes = [vp]
         L.h264o_enc_set_frame_skip.argtypes = [vp, ctypes.c_int]
         L.h264o_enc_frames_skipped.argtypes = [vp]
+        L.h264o_enc_me_stats.argtypes = [vp, vp]
         L.h264o_rc_init_qp.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.h264o_rc_next_qp.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
         L.h264o_write_sps.restype = ctypes.c_size_t

@@ -94,6 +94,23 @@ def test_frame_skip_and_row_qp_in_stream(oracle):
     assert all(len(oe2.encode(f)) > 0 for f in frames)
 
 
+def test_motion_search_stages_exercised(oracle):
+    """the fixture workloads reach every integer-search stage the GPU is held bit-exact on: start
+    points won by a neighbour's vector, cross searches, and cross searches that move the vector"""
+    from h264mi.synth import SyntheticStream
+    tot = np.zeros(3, np.int64)
+    for sid, (w, h, br) in enumerate([(352, 288, 2000000), (640, 360, 1000000), (352, 288, 30000000)]):
+        g = SyntheticStream(sid, w, h)
+        oe = oracle.encoder(w, h, br)
+        oe.set_frame_skip(False)
+        for t in range(5):
+            oe.encode(np.ascontiguousarray(g.frame(t)))
+        st = np.zeros(3, np.int32)
+        oracle.L.h264o_enc_me_stats(oe.e, st.ctypes.data)
+        tot += st
+    assert (tot > 0).all(), tot
+
+
 def test_parameter_sets_are_baseline(oracle):
     buf = np.zeros(64, np.uint8)
     n = oracle.L.h264o_write_sps(1920, 1080, buf.ctypes.data)
