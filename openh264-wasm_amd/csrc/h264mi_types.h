@@ -132,9 +132,15 @@ struct DecState {
 // call k.
 #define H264MI_MAX_NALS 32
 struct NalEnt { int32_t start, end, type; uint32_t stop; };  // header byte index, payload end, type, RBSP stop-bit index
-struct DecFrame {          // per (frame slot, stream): written by dec_scan_kernel and dec_parse_kernel
+struct DecFrame {          // per (frame slot, stream): written by dec_scan_kernel, dec_hdr_kernel, dec_parse_kernel
     const uint8_t *nal;
     int32_t nbytes, nnal, slice, err, got_pic, dbk_idc;
+    // slice header results (dec_hdr_kernel) for the slice-data pass
+    int32_t hdr_ok;        // parameter sets and slice header parsed, slice data to follow
+    int32_t slt;           // slice_type % 5 (0 P, 2 I)
+    int32_t qp, cqp;       // SliceQPY, chroma_qp_index_offset
+    uint32_t data_pos;     // RBSP bit index of slice_data()
+    int32_t pad_h[3];
     NalEnt e[H264MI_MAX_NALS];
 };
 struct DecInput { const uint8_t *nal; const int32_t *size_dev; int32_t size, pad; };  // one access unit

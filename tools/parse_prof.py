@@ -1,7 +1,11 @@
 """Parse-kernel section profile: S streams of 1080p IPPP encoded on the GPU and decoded with
 H264MI_PARSE_PROF=1; prints cycles per section per frame.   usage: parse_prof.py [w h br S nf]"""
 import ctypes, os, sys
-os.environ['H264MI_PARSE_PROF'] = '1'
+PMC = '--pmc' in sys.argv  # plain kernel (no section timers), for rocprofv3 counter passes
+if PMC:
+    sys.argv.remove('--pmc')
+else:
+    os.environ['H264MI_PARSE_PROF'] = '1'
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
@@ -13,9 +17,10 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
     from h264mi.synth import SyntheticStream
     gens = [SyntheticStream(s, w, h) for s in range(S)]
     enc = h264mi.BatchEncoder(w, h, br, S)
+    enc.set_frame_skip(False)  # every frame coded, as in bench.py
     dec = h264mi.BatchDecoder(w, h, S)
     L = h264mi.lib()
-    names = ['-', 'startcode', 'ep-prepass', 'ring-fill', 'skip-runs', 'mb-hdr/pred', 'residual', 'record']
+    names = ['-', '-', '-', 'ring-fill', 'skip-runs', 'mb-hdr', 'residual-rest', 'record', 'qp+ctx', 'luma', 'chromaDC', 'chromaAC']
     prev = np.zeros(S * 16, np.uint64)
     for t in range(nf):
         frames = torch.from_numpy(np.concatenate([g.frame(t) for g in gens])).cuda()
@@ -26,13 +31,17 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
         dec.decode_dev(enc.nal_ptrs(), enc.nal_size_ptrs())
         rc, got = dec.status()
         dt = time.perf_counter() - t0
+        if PMC:
+            print(f'frame {t}: {sizes[0]} B rc={rc} decode {dt*1e3:.2f} ms', flush=True)
+            continue
         cur = np.zeros(S * 16, np.uint64)
         L.h264mi_dec_parse_profile(dec._d, cur.ctypes.data)
         d = (cur - prev).reshape(S, 16)[0]
         prev = cur
-        tot = int(d[1:8].sum())
+        tot = int(d[3:12].sum())
         print(f'frame {t}: {sizes[0]} B rc={rc} decode {dt*1e3:.2f} ms; stream0 cycles total {tot/1e6:.2f} M: ' +
-              ', '.join(f'{names[k]} {int(d[k])/1e6:.2f}M' for k in range(1, 8)), flush=True)
+              ', '.join(f'{names[k]} {int(d[k])/1e6:.2f}M' for k in range(3, 12)) +
+              f'; AC blocks generic {int(d[12])} (sum tc {int(d[15])}), planes skipped {int(d[13])}, blocks skipped {int(d[14])}', flush=True)
 
 
 if __name__ == '__main__':
