@@ -33,6 +33,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
+# Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
+# three entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues two parse streams
+# share one queue and their kernels serialise. Must be set before the HIP runtime initialises.
+if int(os.environ.get('GPU_MAX_HW_QUEUES', '4') or 4) < 8:
+    os.environ['GPU_MAX_HW_QUEUES'] = '8'
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = '1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264'
@@ -51,7 +56,7 @@ def parse():
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
     ap.add_argument('--group', type=int, default=4, help='frames per stream per decode call (frame-parallel entropy decoding)')
-    ap.add_argument('--stages', type=int, default=3, help='NAL staging buffers (groups in flight between encoder and decoder)')
+    ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')

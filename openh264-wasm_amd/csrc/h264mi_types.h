@@ -116,7 +116,7 @@ struct DecParams {          // SPS/PPS fields the slice layer needs (7.3.2.1, 7.
 };
 struct DecState {
     DecParams ps;          // parameter sets of the picture last reconstructed (host reads crop)
-    DecParams psb[2];      // parse-stream chain: call k reads psb[k & 1], its last wave writes psb[~k & 1]
+    DecParams psb[2];      // header chain: call k's dec_hdr_kernel reads psb[k & 1], its last wave writes psb[~k & 1]
     int32_t has_ref;       // reconstruction-side: a reference picture exists
     int32_t got_pic;       // 1 if the frame being (or last) reconstructed produced a picture
     int32_t dbk_idc;       // disable_deblocking_filter_idc of that frame
@@ -127,9 +127,9 @@ struct DecState {
 
 // One decode call processes up to G frames per stream. Entropy decoding of a frame does not depend
 // on other frames' pixels, so all G x S slices are parsed concurrently (one wave each); the
-// reconstruction / deblocking passes then run frame by frame. Parsing runs on its own HIP stream
-// into one of two halves of 2G frame slots, so the parse of call k+1 overlaps the reconstruction of
-// call k.
+// reconstruction / deblocking passes then run frame by frame. Calls take G-slot groups of a ring of
+// frame slots in turn and parse on two alternating HIP streams, so the slice data of consecutive
+// calls is entropy-decoded concurrently while earlier calls reconstruct (runtime_dec.inc).
 #define H264MI_MAX_NALS 32
 struct NalEnt { int32_t start, end, type; uint32_t stop; };  // header byte index, payload end, type, RBSP stop-bit index
 struct DecFrame {          // per (frame slot, stream): written by dec_scan_kernel, dec_hdr_kernel, dec_parse_kernel
@@ -141,6 +141,7 @@ struct DecFrame {          // per (frame slot, stream): written by dec_scan_kern
     int32_t qp, cqp;       // SliceQPY, chroma_qp_index_offset
     uint32_t data_pos;     // RBSP bit index of slice_data()
     int32_t pad_h[3];
+    DecParams ps;          // parameter sets in effect for this frame's slice (cropping for the output)
     NalEnt e[H264MI_MAX_NALS];
 };
 struct DecInput { const uint8_t *nal; const int32_t *size_dev; int32_t size, pad; };  // one access unit

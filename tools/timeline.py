@@ -1,41 +1,16 @@
-"""Overlap analysis of a rocprofv3 kernel trace (the bench's timed region): per kernel name the busy
-time, and for the last N ms of the trace how much of the wall time had each kernel running and how
-much had >= 2 of the codec kernels running at once.   usage: timeline.py <trace.csv> [window_ms]"""
+"""Kernel timeline of the last `steps` encoder steps of a bench trace: every dispatch with its HIP
+stream, start and end relative to the first timed enc_mb_kernel (ms), to see what serialises.
+usage: timeline.py <kernel_trace.csv> [steps] [filter-substring ...]"""
 import csv, sys
-from collections import defaultdict
-
-rows = []
-for r in csv.DictReader(open(sys.argv[1])):
-    n = r['Kernel_Name']
-    if 'h264mi::' not in n:
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+flt = sys.argv[3:] or ['enc_mb_kernel', 'dec_parse_kernel', 'dec_recon_kernel', 'dec_hdr', 'dec_scan', 'enc_copy']
+ks = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0].replace('h264mi::', ''), r.get('Stream_Id', r.get('Queue_Id', '?')), r.get('Queue_Id', '?')) for r in rows)
+mb = [k for k in ks if k[2] == 'enc_mb_kernel']
+t0 = mb[-steps][0]
+tend = max(k[1] for k in ks)
+print(f'from first timed enc_mb_kernel to last kernel end: {(tend - t0) / 1e6:.2f} ms')
+for s, e, n, st, q in ks:
+    if e < t0 or not any(f in n for f in flt):
         continue
-    rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), n.split('h264mi::')[1].split('(')[0]))
-rows.sort()
-end = max(e for _, e, _ in rows)
-win = float(sys.argv[2]) if len(sys.argv) > 2 else 500.0
-t0 = end - win * 1e6
-rows = [(max(s, t0), e, n) for s, e, n in rows if e > t0]
-ev = []
-for s, e, n in rows:
-    ev.append((s, 1, n)); ev.append((e, -1, n))
-ev.sort()
-active = defaultdict(int)
-busy = defaultdict(float)
-multi = 0.0
-anyb = 0.0
-last = t0
-for t, d, n in ev:
-    dt = t - last
-    names = [k for k, v in active.items() if v > 0]
-    for k in names:
-        busy[k] += dt
-    if names:
-        anyb += dt
-    if len(names) >= 2:
-        multi += dt
-    active[n] += d
-    last = t
-W = end - t0
-print(f'window {W / 1e6:.1f} ms: any kernel {anyb / W:.1%}, >=2 kernels {multi / W:.1%}')
-for k, v in sorted(busy.items(), key=lambda kv: -kv[1]):
-    print(f'  {k:28s} running {v / W:6.1%} of wall')
+    print(f'{(s - t0) / 1e6:9.3f} {(e - t0) / 1e6:9.3f}  dur {(e - s) / 1e6:8.3f}  stream {st} queue {q}  {n}')
