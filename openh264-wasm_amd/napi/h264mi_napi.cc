@@ -17,49 +17,9 @@
 #include <cstring>
 #include <map>
 #include "../../include/h264mi.h"
+#include "heap.h"
 
 namespace {
-
-struct Heap {
-    uint8_t *base = nullptr;
-    size_t size = 0;
-    std::map<uint32_t, uint32_t> free_;  // offset -> bytes (coalesced)
-    std::map<uint32_t, uint32_t> used_;
-    void init(uint8_t *b, size_t n) {
-        base = b; size = n;
-        free_.clear(); used_.clear();
-        if (n > 16) free_[16] = (uint32_t)(n - 16);
-    }
-    uint32_t alloc(size_t n) {
-        if (n == 0) n = 1;
-        const uint32_t need = (uint32_t)((n + 15) & ~(size_t)15);
-        for (auto it = free_.begin(); it != free_.end(); ++it) {
-            if (it->second < need) continue;
-            const uint32_t off = it->first, rest = it->second - need;
-            free_.erase(it);
-            if (rest) free_[off + need] = rest;
-            used_[off] = need;
-            return off;
-        }
-        return 0;
-    }
-    void release(uint32_t off) {
-        auto u = used_.find(off);
-        if (u == used_.end()) return;
-        uint32_t o = off, n = u->second;
-        used_.erase(u);
-        auto nx = free_.lower_bound(o);
-        if (nx != free_.end() && nx->first == o + n) { n += nx->second; free_.erase(nx); }
-        auto pv = free_.lower_bound(o);
-        if (pv != free_.begin()) {
-            --pv;
-            if (pv->first + pv->second == o) { o = pv->first; n += pv->second; free_.erase(pv); }
-        }
-        free_[o] = n;
-    }
-    bool ok(int64_t off, int64_t n) const { return off > 0 && n >= 0 && (uint64_t)(off + n) <= size; }
-    uint8_t *at(int64_t off) const { return base + off; }
-};
 
 struct EnvData {
     Heap heap;
@@ -93,7 +53,8 @@ bool args(napi_env env, napi_callback_info info, int64_t *v, size_t n) {
             napi_throw_type_error(env, nullptr, "h264mi: arguments are numbers (heap offsets / ints)");
             return false;
         }
-        v[i] = (int64_t)x;
+        // NaN / +-Inf / |x| > 2^53 become -1 (rejected by every bounds check) instead of an undefined conversion
+        v[i] = (x == x && x >= -9007199254740992.0 && x <= 9007199254740992.0) ? (int64_t)x : -1;
     }
     return true;
 }
@@ -157,8 +118,9 @@ template <bool RGBA> napi_value js_encode(napi_env env, napi_callback_info info)
     Heap &h = d->heap;
     put_i32(h, a[3], 0);
     put_i32(h, a[4], 0);
+    if (a[1] <= 0 || a[2] <= 0 || a[1] > 16384 || a[2] > 16384) return undef(env);  // (the product cannot overflow)
     const int64_t in_bytes = RGBA ? a[1] * a[2] * 4 : a[1] * a[2] * 3 / 2;
-    if (a[1] <= 0 || a[2] <= 0 || !h.ok(a[0], in_bytes) || !h.ok(a[3], 4) || !h.ok(a[4], 4)) return undef(env);
+    if (!h.ok(a[0], in_bytes) || !h.ok(a[3], 4) || !h.ok(a[4], 4)) return undef(env);
     unsigned char *out = nullptr;
     int n = 0;
     if (RGBA) h264mi_i_encode_frame(d->inst, h.at(a[0]), (int)a[1], (int)a[2], &out, &n);

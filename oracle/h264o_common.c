@@ -147,7 +147,7 @@ void dequant_block(const int16_t lvl[16], int qp, int first, int out[16]) {
     for (int k = 0; k < 16; k++) out[k] = 0;
     for (int k = first; k < 16; k++) {
         int pos = ZIGZAG4[k];
-        out[pos] = (lvl[k] * DEQUANT_V[qp % 6][POS_CLASS[pos]]) << (qp / 6);
+        out[pos] = lvl[k] * DEQUANT_V[qp % 6][POS_CLASS[pos]] * (1 << (qp / 6));
     }
 }
 /* 8.5.10: inverse Hadamard of Intra16x16 DC + scaling. Output raster over 4x4 block grid. */
@@ -165,7 +165,7 @@ void luma_dc_dequant(const int16_t lvl[16], int qp, int dc[16]) {
         int f[4] = {a + b + e + d, a + b - e - d, a - b - e + d, a - b + e - d};
         for (int i = 0; i < 4; i++) {
             int x = f[i] * v;
-            dc[4 * i + j] = q6 >= 2 ? (x << (q6 - 2)) : ((x + (1 << (1 - q6))) >> (2 - q6));
+            dc[4 * i + j] = q6 >= 2 ? x * (1 << (q6 - 2)) : ((x + (1 << (1 - q6))) >> (2 - q6));
         }
     }
 }
@@ -174,8 +174,8 @@ void chroma_dc_dequant(const int16_t l[4], int qpc, int dc[4]) {
     int f0 = l[0] + l[1] + l[2] + l[3], f1 = l[0] - l[1] + l[2] - l[3];
     int f2 = l[0] + l[1] - l[2] - l[3], f3 = l[0] - l[1] - l[2] + l[3];
     int v = DEQUANT_V[qpc % 6][0], q6 = qpc / 6;
-    dc[0] = ((f0 * v) << q6) >> 1; dc[1] = ((f1 * v) << q6) >> 1;
-    dc[2] = ((f2 * v) << q6) >> 1; dc[3] = ((f3 * v) << q6) >> 1;
+    dc[0] = (f0 * v * (1 << q6)) >> 1; dc[1] = (f1 * v * (1 << q6)) >> 1;
+    dc[2] = (f2 * v * (1 << q6)) >> 1; dc[3] = (f3 * v * (1 << q6)) >> 1;
 }
 
 /* ================= intra prediction ================= */
@@ -471,13 +471,13 @@ static void filter_line(uint8_t *q, int st, int bS, int alpha, int beta, int tc0
     if (bS < 4) {
         if (chroma) {
             int tc = tc0 + 1;
-            int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+            int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
             q[-st] = (uint8_t)clip1(p0 + d); q[0] = (uint8_t)clip1(q0 - d);
         } else {
             int p2 = q[-3 * st], q2 = q[2 * st];
             int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
             int tc = tc0 + (ap < beta) + (aq < beta);
-            int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+            int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
             q[-st] = (uint8_t)clip1(p0 + d); q[0] = (uint8_t)clip1(q0 - d);
             if (ap < beta) q[-2 * st] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
             if (aq < beta) q[st] = (uint8_t)(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));

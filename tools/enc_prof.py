@@ -13,6 +13,7 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
     from h264mi.synth import SyntheticStream
     gens = [SyntheticStream(s, w, h) for s in range(S)]
     enc = h264mi.BatchEncoder(w, h, br, S)
+    enc.set_frame_skip(False)  # every frame coded, as in bench.py
     L = h264mi.lib()
     names = ['row-start-wait', 'wait-above', 'loads+ctx', 'pskip-test', 'int-ME', 'subpel', 'intra-alt', 'p16-resid', 'I4-search',
              'I-resid', 'outputs', 'F:pskip-pred', 'F:ME-first', 'F:satd-half', 'F:sel+satd-q', 'F:p16-pred']

@@ -1,6 +1,9 @@
 """Parse-kernel section profile: S streams of 1080p IPPP encoded on the GPU and decoded with
 H264MI_PARSE_PROF=1; prints cycles per section per frame.   usage: parse_prof.py [w h br S nf]"""
 import ctypes, os, sys
+LOAD = '--load' in sys.argv  # an 8-stream encoder runs on another HIP stream while decoding (the bench's mix)
+if LOAD:
+    sys.argv.remove('--load')
 PMC = '--pmc' in sys.argv  # plain kernel (no section timers), for rocprofv3 counter passes
 if PMC:
     sys.argv.remove('--pmc')
@@ -19,6 +22,12 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
     enc = h264mi.BatchEncoder(w, h, br, S)
     enc.set_frame_skip(False)  # every frame coded, as in bench.py
     dec = h264mi.BatchDecoder(w, h, S)
+    if LOAD:
+        es = torch.cuda.Stream()
+        lenc = h264mi.BatchEncoder(w, h, br, 8, stream=es)
+        lenc.set_frame_skip(False)
+        lgen = [SyntheticStream(100 + s, w, h) for s in range(8)]
+        lclip = [torch.from_numpy(np.concatenate([g.frame(t) for g in lgen])).cuda() for t in range(4)]
     L = h264mi.lib()
     names = ['-', '-', '-', 'ring-fill', 'skip-runs', 'mb-hdr', 'residual-rest', 'record', 'qp+ctx', 'luma', 'chromaDC', 'chromaAC']
     NSL = S * max(2, min(8, 32 // 1))  # frame slots of a max_frames=1 decoder (runtime_dec.inc: NG groups)
@@ -28,6 +37,10 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
         enc.encode(frames)
         sizes = enc.nal_sizes()
         torch.cuda.synchronize()
+        if LOAD:
+            with torch.cuda.stream(es):
+                for k in range(12):
+                    lenc.encode(lclip[k % 4])
         t0 = time.perf_counter()
         dec.decode_dev(enc.nal_ptrs(), enc.nal_size_ptrs())
         rc, got = dec.status()
@@ -40,9 +53,10 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
         d = (cur - prev).reshape(-1, S, 16).sum(0)[0]
         prev = cur
         tot = int(d[3:12].sum())
+        mhz = d[1] / d[0] * 100 if d[0] else 0
         print(f'frame {t}: {sizes[0]} B rc={rc} decode {dt*1e3:.2f} ms; stream0 cycles total {tot/1e6:.2f} M: ' +
               ', '.join(f'{names[k]} {int(d[k])/1e6:.2f}M' for k in range(3, 12)) +
-              f'; AC blocks generic {int(d[12])} (sum tc {int(d[15])}), planes skipped {int(d[13])}, blocks skipped {int(d[14])}', flush=True)
+              f'; slice {int(d[0]) / 1e5:.2f} ms at {mhz:.0f} MHz; AC blocks generic {int(d[12])} (sum tc {int(d[15])}), planes skipped {int(d[13])}, blocks skipped {int(d[14])}', flush=True)
 
 
 if __name__ == '__main__':
