@@ -33,11 +33,6 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
-# Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
-# three entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues two parse streams
-# share one queue and their kernels serialise. Must be set before the HIP runtime initialises.
-if int(os.environ.get('GPU_MAX_HW_QUEUES', '4') or 4) < 8:
-    os.environ['GPU_MAX_HW_QUEUES'] = '8'
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = '1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264'
@@ -57,6 +52,7 @@ def parse():
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
     ap.add_argument('--group', type=int, default=4, help='frames per stream per decode call (frame-parallel entropy decoding)')
     ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
+    ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
@@ -66,6 +62,12 @@ def parse():
         a.width, a.height = a.width or 1280, a.height or 720
     a.width, a.height = a.width or 1920, a.height or 1080
     a.streams = a.streams or {3: 1, 5: 4}.get(a.config, 8)
+    # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
+    # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
+    # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
+    need = max(8, a.parse_streams + 5)
+    if int(os.environ.get('GPU_MAX_HW_QUEUES', '4') or 4) < need:
+        os.environ['GPU_MAX_HW_QUEUES'] = str(min(need, 32))
     return a
 
 
@@ -244,6 +246,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # the rate control's buffer and most frames would be dropped)
     enc.set_frame_skip(False)
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G) if decode else None
+    if dec is not None and a.parse_streams != 3:
+        dec.set_parse_streams(a.parse_streams)
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
@@ -311,6 +315,11 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         pms, pn = dec.kernel_time(1)
         kern['dec_recon_kernel'] = {'avg_ms': rms / max(rn, 1), 'launches': rn}
         kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': S * G}
+        if os.environ.get('H264MI_PARSE_PROF'):  # diagnostic: the slices' own duration (wave start to end)
+            nsl = S * G * max(2, min(8, 32 // G))
+            prof = np.zeros(nsl * 16, np.uint64)
+            h264mi.lib().h264mi_dec_parse_profile(dec._d, prof.ctypes.data)
+            kern['dec_parse_kernel']['slice_ms_mean_all_calls'] = float(prof.reshape(-1, 16)[:, 0].sum()) / 1e5 / max(1, (a.warmup + a.steps) * S)
     sizes = enc.nal_sizes()
     # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
     # (read source F + read reference F + write reconstruction F) for a P frame, 2F for an IDR
@@ -353,6 +362,8 @@ def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
     nbytes = usz.cpu().tolist()
     ds = torch.cuda.Stream(device=dev)
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
+    if a.parse_streams != 3:
+        dec.set_parse_streams(a.parse_streams)
     state = {'t': 0}
 
     def run_steps(k):

@@ -107,6 +107,9 @@ h264mi_decoder *h264mi_dec_create(int width, int height, int nstreams, void *hip
    reconstructed in order; after the call each stream's picture is that of its last frame. */
 h264mi_decoder *h264mi_dec_create_batch(int width, int height, int nstreams, int max_frames, void *hip_stream);
 int h264mi_dec_max_frames(h264mi_decoder *d);
+/* number of HIP streams the entropy decoding of consecutive calls rotates over (default 3, 1..16):
+   up to that many calls are entropy-decoded concurrently; synchronises the decoder */
+int h264mi_dec_set_parse_streams(h264mi_decoder *d, int nstreams);
 void h264mi_dec_destroy(h264mi_decoder *d);
 /* async; d_nal[s] / nal_bytes[s] (host array) per stream; a stream with nal_bytes 0 is skipped */
 int h264mi_dec_decode(h264mi_decoder *d, const void *const *d_nal, const int *nal_bytes);

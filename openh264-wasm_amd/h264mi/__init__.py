@@ -67,6 +67,7 @@ def lib():
             'h264mi_dec_decode_frames_after_n': (i, [vp, i, vp, vp, vp, vp, i]),
             'h264mi_dec_recon_profile': (i, [vp, vp]),
             'h264mi_dec_max_frames': (i, [vp]),
+            'h264mi_dec_set_parse_streams': (i, [vp, i]),
             'h264mi_dec_decode': (i, [vp, vp, vp]),
             'h264mi_dec_sync': (i, [vp]),
             'h264mi_dec_set_timing': (i, [vp, i]),
@@ -318,6 +319,10 @@ class BatchDecoder:
         ev = (ctypes.c_void_p * max(1, len(evs)))(*[e.cuda_event for e in evs])
         if self._L.h264mi_dec_decode_frames_after_n(self._d, m // self.S, ptrs, sizes, sp, ev, len(evs)) != 0:
             raise RuntimeError('h264mi_dec_decode_frames failed')
+
+    def set_parse_streams(self, n):
+        if self._L.h264mi_dec_set_parse_streams(self._d, n) != 0:
+            raise RuntimeError('h264mi_dec_set_parse_streams failed')
 
     def set_timing(self, on):
         self._L.h264mi_dec_set_timing(self._d, 1 if on else 0)
