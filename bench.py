@@ -53,6 +53,9 @@ def parse():
     ap.add_argument('--group', type=int, default=4, help='frames per stream per decode call (frame-parallel entropy decoding)')
     ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
+    ap.add_argument('--parse-cus', type=int, default=-1,
+                    help='CUs reserved for entropy decoding (CU mask bits [0, n) for the parse streams, the rest for the '
+                         'encoder / reconstruction streams); 0 = shared; default 16 when encoding and decoding, else 0')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
@@ -62,6 +65,8 @@ def parse():
         a.width, a.height = a.width or 1280, a.height or 720
     a.width, a.height = a.width or 1920, a.height or 1080
     a.streams = a.streams or {3: 1, 5: 4}.get(a.config, 8)
+    if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
+        a.parse_cus = 16 if a.config in (0, 3, 5) else 0
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
@@ -240,7 +245,10 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # on `ds`, takes G frames per call, entropy-decoding all G x S slices concurrently before
     # reconstructing them in order. NB staging buffers keep NB groups in flight: encoding group g+1
     # overlaps the entropy decoding of g and the reconstruction of g-1.
-    es, ds = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    if a.parse_cus > 0:  # wavefront streams off the CUs reserved for entropy decoding
+        es, ds = h264mi.masked_stream(0, a.parse_cus, True), h264mi.masked_stream(0, a.parse_cus, True)
+    else:
+        es, ds = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
     enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
     # frame skipping off: every step codes a frame (at 1 Mbps the synthetic 1080p content overflows
     # the rate control's buffer and most frames would be dropped)
@@ -248,6 +256,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G) if decode else None
     if dec is not None and a.parse_streams != 3:
         dec.set_parse_streams(a.parse_streams)
+    if dec is not None and a.parse_cus > 0:
+        dec.set_parse_cus(0, a.parse_cus)
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
@@ -331,6 +341,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                        + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
            'baseline_config': {0: 'metric (configs[2] x 8 streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
+           'parse_cus': a.parse_cus, 'parse_streams': a.parse_streams,
            'parallelism': f'streams x{world} (weak)'}
     return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg,
             'roofline': roofline('enc_mb_kernel', alg, ems, en, a), 'kernels': kern,
@@ -360,10 +371,12 @@ def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
         enc.copy_nals(units[t], slot, usz[t:t + 1])
     sync()
     nbytes = usz.cpu().tolist()
-    ds = torch.cuda.Stream(device=dev)
+    ds = h264mi.masked_stream(0, a.parse_cus, True) if a.parse_cus > 0 else torch.cuda.Stream(device=dev)
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G)
     if a.parse_streams != 3:
         dec.set_parse_streams(a.parse_streams)
+    if a.parse_cus > 0:
+        dec.set_parse_cus(0, a.parse_cus)
     state = {'t': 0}
 
     def run_steps(k):

@@ -110,6 +110,13 @@ int h264mi_dec_max_frames(h264mi_decoder *d);
 /* number of HIP streams the entropy decoding of consecutive calls rotates over (default 3, 1..16):
    up to that many calls are entropy-decoded concurrently; synchronises the decoder */
 int h264mi_dec_set_parse_streams(h264mi_decoder *d, int nstreams);
+/* entropy decoding on reserved CUs: the parse streams get the CU mask bits [cu_lo, cu_hi) (the runtime
+   stripes mask bits over the XCDs); cu_lo == cu_hi removes the mask. Pair with wavefront streams from
+   h264mi_stream_create_cus(cu_lo, cu_hi, 1) so that encoder / reconstruction workgroups stay off them. */
+int h264mi_dec_set_parse_cus(h264mi_decoder *d, int cu_lo, int cu_hi);
+/* a HIP stream restricted to CU mask bits [cu_lo, cu_hi), or to every other CU when complement != 0 */
+void *h264mi_stream_create_cus(int cu_lo, int cu_hi, int complement);
+void h264mi_stream_destroy(void *hip_stream);
 void h264mi_dec_destroy(h264mi_decoder *d);
 /* async; d_nal[s] / nal_bytes[s] (host array) per stream; a stream with nal_bytes 0 is skipped */
 int h264mi_dec_decode(h264mi_decoder *d, const void *const *d_nal, const int *nal_bytes);

@@ -68,6 +68,9 @@ def lib():
             'h264mi_dec_recon_profile': (i, [vp, vp]),
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_set_parse_streams': (i, [vp, i]),
+            'h264mi_dec_set_parse_cus': (i, [vp, i, i]),
+            'h264mi_stream_create_cus': (vp, [i, i, i]),
+            'h264mi_stream_destroy': (None, [vp]),
             'h264mi_dec_decode': (i, [vp, vp, vp]),
             'h264mi_dec_sync': (i, [vp]),
             'h264mi_dec_set_timing': (i, [vp, i]),
@@ -275,6 +278,16 @@ class BatchEncoder:
             pass
 
 
+def masked_stream(cu_lo, cu_hi, complement=False):
+    """A torch stream (ExternalStream over h264mi_stream_create_cus) restricted to CU mask bits
+    [cu_lo, cu_hi), or to every other CU. Pairs with BatchDecoder.set_parse_cus."""
+    import torch
+    h = lib().h264mi_stream_create_cus(cu_lo, cu_hi, 1 if complement else 0)
+    if not h:
+        raise RuntimeError('h264mi_stream_create_cus failed')
+    return torch.cuda.ExternalStream(h)
+
+
 class BatchDecoder:
     """S independent decoder streams of one geometry; NAL units in HBM. max_frames > 1 enables
     decode_frames(): several access units per stream per call, entropy-decoded concurrently."""
@@ -319,6 +332,11 @@ class BatchDecoder:
         ev = (ctypes.c_void_p * max(1, len(evs)))(*[e.cuda_event for e in evs])
         if self._L.h264mi_dec_decode_frames_after_n(self._d, m // self.S, ptrs, sizes, sp, ev, len(evs)) != 0:
             raise RuntimeError('h264mi_dec_decode_frames failed')
+
+    def set_parse_cus(self, lo, hi):
+        """entropy decoding on CU mask bits [lo, hi) (see h264mi_dec_set_parse_cus)"""
+        if self._L.h264mi_dec_set_parse_cus(self._d, lo, hi) != 0:
+            raise RuntimeError('h264mi_dec_set_parse_cus failed')
 
     def set_parse_streams(self, n):
         if self._L.h264mi_dec_set_parse_streams(self._d, n) != 0:
