@@ -18,7 +18,9 @@ sys.path.insert(0, os.path.join(ROOT, 'tools'))
     (352, 288, 2000000, 2, 10, 1, 4),    # 4-frame batches, device sizes, ragged tail
     (208, 120, 500000, 3, 7, 0, 3),      # cropped geometry, host sizes
     (1920, 1080, 1000000, 4, 6, 1, 3),   # bench geometry
-], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3'])
+    (352, 288, 2000000, 3, 9, 1, 3, 16),    # reserved decode lane: parse on 16 masked CUs, wavefronts on the rest
+    (1920, 1080, 1000000, 4, 6, 1, 2, 16),  # the same at the bench geometry
+], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3', 'cif-lanes16', '1080p-lanes16'])
 def test_batch_encode_decode(gpu_lib, args):
     import batch_check
     assert batch_check.main(*args)

@@ -2,14 +2,16 @@
 BatchDecoder. With group G = 1 every frame is decoded right after it is encoded (decode or
 decode_dev); with G > 1 frames are staged and decoded G at a time (decode_frames). Checks per
 decode call: decoder status, decoder picture == encoder reconstruction (every stream), and stream
-0's bytes == oracle bytes for every frame.   usage: batch_check.py w h br S nf [dev=1] [G=1]"""
+0's bytes == oracle bytes for every frame. lanes > 0: encoder and reconstruction on streams masked off
+CU bits [0, lanes), entropy decoding (4 parse streams) on those CUs -- the bench's reserved decode lane.
+usage: batch_check.py w h br S nf [dev=1] [G=1] [lanes=0]"""
 import ctypes, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
 
 
-def main(w, h, br, S, nf, dev=1, G=1):
+def main(w, h, br, S, nf, dev=1, G=1, lanes=0):
     import torch
     import h264mi
     from h264mi.synth import SyntheticStream
@@ -19,9 +21,13 @@ def main(w, h, br, S, nf, dev=1, G=1):
     O.h264o_enc_set_frame_skip(oe, 0)  # the batch pipeline under test decodes every frame
     F = w * h * 3 // 2
     gens = [SyntheticStream(s, w, h) for s in range(S)]
-    enc = h264mi.BatchEncoder(w, h, br, S)
+    st = h264mi.masked_stream(0, lanes, True) if lanes else None
+    enc = h264mi.BatchEncoder(w, h, br, S, stream=st)
     enc.set_frame_skip(False)
-    dec = h264mi.BatchDecoder(w, h, S, max_frames=G)
+    dec = h264mi.BatchDecoder(w, h, S, stream=st, max_frames=G)
+    if lanes:
+        dec.set_parse_streams(4)
+        dec.set_parse_cus(0, lanes)
     out = np.zeros(w * h * 4, np.uint8)
     slot = 1 << 21
     stage = torch.empty((G, S * slot), dtype=torch.uint8, device='cuda')
@@ -34,7 +40,8 @@ def main(w, h, br, S, nf, dev=1, G=1):
         sizes = None
         for j in range(n):
             host = np.concatenate([g.frame(t + j) for g in gens])
-            enc.encode(torch.from_numpy(host).cuda())
+            with torch.cuda.stream(st) if st is not None else torch.cuda.stream(torch.cuda.current_stream()):
+                enc.encode(torch.from_numpy(host).cuda())
             sizes = enc.nal_sizes()
             m = O.h264o_enc_encode(oe, host[:F].ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(out.size))
             same0 = same0 and enc.nal_bytes(0, sizes[0]) == out[:m].tobytes()
@@ -47,6 +54,8 @@ def main(w, h, br, S, nf, dev=1, G=1):
                 dec.decode(enc.nal_ptrs(), sizes)
         else:
             torch.cuda.synchronize()
+            if st is not None:
+                st.synchronize()
             ptrs = [stage.data_ptr() + j * S * slot + s * slot for j in range(n) for s in range(S)]
             if dev:
                 szp = [stage_sz.data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
