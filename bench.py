@@ -237,9 +237,6 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
-    parity_ok, parity_msg = True, 'skipped (--no-cpu-baseline or N > 1)'
-    if cpu is not None:
-        parity_ok, parity_msg = gpu_parity(a, cpu.get('parity_hashes'), i_only=a.config == 2)
     W, H, S, G = a.width, a.height, a.streams, a.group
     F = W * H * 3 // 2
     sync = torch.cuda.synchronize
@@ -248,6 +245,11 @@ def main():
         res = bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync)
     else:
         res = bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank)
+    # the oracle parity check runs after the timed region: its own encoder and decoder (and their HIP
+    # streams) would otherwise exist before the timed pipeline's streams are created
+    parity_ok, parity_msg = True, 'skipped (--no-cpu-baseline or N > 1)'
+    if cpu is not None:
+        parity_ok, parity_msg = gpu_parity(a, cpu.get('parity_hashes'), i_only=a.config == 2)
     parity_ok = parity_ok and res.pop('selfcheck_ok')
     elapsed = res.pop('elapsed')
     if dist:
