@@ -254,6 +254,23 @@ DEV void wave_lds_sync() { asm volatile("" ::: "memory"); }
 template <class P> DEV void gran_store(P g, uint32_t epoch, uint32_t v) {
     __hip_atomic_store(g, ((uint64_t)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// two consecutive granules {epoch, a}, {epoch, b} from one lane: one 16-byte write-through (sc1) store
+// (cdna_hip_programming.md Guideline 16 R1 store form; each 8-byte half is a complete granule, which
+// consumers poll as before). Halves the store instructions of a granule hand-off. base: wave-uniform
+// (the buffer descriptor lives in SGPRs), idx: the lane's first granule, even.
+#ifndef H264MI_GRAN16
+#define H264MI_GRAN16 1
+#endif
+template <class P> DEV void gran_store2(P base, int idx, uint32_t epoch, uint32_t a, uint32_t b) {
+#if H264MI_GRAN16
+    const u32x4 v = {a, epoch, b, epoch};
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(uint64_t)base, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, idx * 8, 0, 16);
+#else
+    gran_store(base + idx, epoch, a);
+    gran_store(base + idx + 1, epoch, b);
+#endif
+}
 // lanes [0, n) each poll one granule; returns false on abort/timeout. Payload of lane's granule in *v.
 template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, int32_t *abort_word) {
     int lane = threadIdx.x & 63;

@@ -5,7 +5,7 @@ set -o pipefail
 out=gpurun_out/$1; shift; mkdir -p $out
 names=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do names+=("$1"); shift; done; [ "$1" = "--" ] && shift
 for n in "${names[@]}"; do
-  for cfg in 0 4; do
+  for cfg in ${CFGS:-0 4}; do
     H264MI_LIB=$PWD/openh264-wasm_amd/lib/variants/$n.so timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 --config $cfg "$@" > $out/$n.c$cfg.log 2>&1 || { echo "$n c$cfg FAILED"; tail -5 $out/$n.c$cfg.log; exit 1; }
     python3 - $out/$n.c$cfg.log $n $cfg <<'PY'
 import json,sys
