@@ -55,7 +55,7 @@ def parse():
     ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
     ap.add_argument('--parse-cus', type=int, default=-1,
                     help='CUs reserved for entropy decoding (CU mask bits [0, n) for the parse streams, the rest for the '
-                         'encoder / reconstruction streams); 0 = shared; default 16 when encoding and decoding, else 0')
+                         'encoder / reconstruction streams); 0 = shared; default 24 when encoding and decoding, else 0')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
@@ -67,7 +67,7 @@ def parse():
     a.width, a.height = a.width or 1920, a.height or 1080
     a.streams = a.streams or {3: 1, 5: 4}.get(a.config, 8)
     if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
-        a.parse_cus = 16 if a.config in (0, 3, 5) else 0
+        a.parse_cus = 24 if a.config in (0, 3, 5) else 0
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
