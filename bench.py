@@ -50,7 +50,9 @@ def parse():
     ap.add_argument('--height', type=int, default=0)
     ap.add_argument('--bitrate', type=int, default=1000000)
     ap.add_argument('--clip', type=int, default=60, help='frames per stream kept resident (IPPP continues across wrap)')
-    ap.add_argument('--group', type=int, default=4, help='frames per stream per decode call (frame-parallel entropy decoding)')
+    ap.add_argument('--group', type=int, default=0,
+                    help='frames per stream per decode call (frame-parallel entropy decoding); default 4, 16 for the '
+                         'decode-only config (no encoder latency to hide: more slices in flight)')
     ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
     ap.add_argument('--parse-cus', type=int, default=-1,
@@ -66,6 +68,7 @@ def parse():
         a.width, a.height = a.width or 1280, a.height or 720
     a.width, a.height = a.width or 1920, a.height or 1080
     a.streams = a.streams or {3: 1, 5: 4}.get(a.config, 8)
+    a.group = a.group or (16 if a.config == 4 else 4)
     if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
         a.parse_cus = 24 if a.config in (0, 3, 5) else 0
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
