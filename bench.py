@@ -35,7 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-METRIC = '1080p30 frames/sec encode+decode per GPU; bit-exact vs OpenH264'
+# BASELINE.json's metric names "bit-exact vs OpenH264"; what this build can show is parity with the oracle
+# (the CPU restatement) -- OpenH264 parity is unpinned, so the line does not claim it
+METRIC = '1080p30 frames/sec encode+decode per GPU'
 PARITY_NOTE = 'NAL bytes and decoded pictures == oracle (CPU restatement) at this config; OpenH264 parity unpinned'
 
 
@@ -107,13 +109,28 @@ TRAFFIC_FRAMES, TRAFFIC_SKIP = 12, 2  # probe frames; dispatches excluded from t
 
 
 def traffic_probe(a):
-    """child of measure_traffic(), run under rocprofv3 --pmc: the bench's encoder alone (S streams,
-    geometry, bitrate, frame skipping off) for TRAFFIC_FRAMES frames; enc_mb_kernel dispatch k = frame k"""
+    """child of measure_traffic(), run under rocprofv3 --pmc. Encoding configs: the bench's encoder alone
+    (S streams, geometry, bitrate, frame skipping off) for TRAFFIC_FRAMES frames; enc_mb_kernel dispatch
+    k = frame k. Config 4: one stream encoded, then decoded frame by frame by S decoders; dec_recon_kernel
+    dispatch k = frame k of all S decoders."""
     import numpy as np
     import torch
     import h264mi
     from h264mi.synth import SyntheticStream
     W, H, S = a.width, a.height, a.streams
+    if a.config == 4:
+        g = SyntheticStream(0, W, H)
+        enc = h264mi.BatchEncoder(W, H, a.bitrate, 1)
+        enc.set_frame_skip(False)
+        dec = h264mi.BatchDecoder(W, H, S)
+        for t in range(TRAFFIC_FRAMES):
+            enc.encode(torch.from_numpy(np.ascontiguousarray(g.frame(t))).cuda())
+            n = enc.nal_sizes()[0]
+            dec.decode([enc.nal_ptr(0)] * S, [n] * S)
+            dec.status()
+        dec.close()
+        enc.close()
+        return
     gens = [SyntheticStream(s, W, H) for s in range(S)]
     enc = h264mi.BatchEncoder(W, H, a.bitrate, S)
     enc.set_frame_skip(False)
@@ -126,10 +143,12 @@ def traffic_probe(a):
 
 
 def measure_traffic(a):
-    """HBM bytes per enc_mb_kernel launch, measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE,
-    then WRITE_SIZE: they do not fit one pass) over a child that runs the bench's encoder, started
+    """HBM bytes per launch of the line's dominant kernel (a.traffic_kernel: enc_mb_kernel, or
+    dec_recon_kernel for config 4), measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, then
+    WRITE_SIZE: they do not fit one pass) over a child that runs the bench's encoder (decoders), started
     before this process touches the GPU. gfx950 (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the
     bytes of wide streaming reads, so read bytes = 2 x FETCH_SIZE; both counters are KiB."""
+    kname = a.traffic_kernel
     import csv
     import glob
     import shutil
@@ -151,21 +170,36 @@ def measure_traffic(a):
         per = {}
         for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
             for r in csv.DictReader(open(f)):
-                if 'enc_mb_kernel' in r['Kernel_Name'] and r['Counter_Name'] == ctr:
+                if kname in r['Kernel_Name'] and r['Counter_Name'] == ctr:
                     per[int(r['Dispatch_Id'])] = per.get(int(r['Dispatch_Id']), 0.0) + float(r['Counter_Value'])
         ks = sorted(per)[TRAFFIC_SKIP:]
         if not ks:
-            return None, f'{ctr}: no enc_mb_kernel dispatches recorded'
+            return None, f'{ctr}: no {kname} dispatches recorded'
         vals[ctr] = sum(per[k] for k in ks) / len(ks)
     shutil.rmtree(work, ignore_errors=True)
     hbm = (2 * vals['FETCH_SIZE'] + vals['WRITE_SIZE']) * 1024
-    return hbm, (f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over enc_mb_kernel dispatches '
-                 f'{TRAFFIC_SKIP}..{TRAFFIC_FRAMES - 1} of the bench encoder; bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 '
-                 f'(read {2 * vals["FETCH_SIZE"] * 1024 / 1e6:.1f} MB, written {vals["WRITE_SIZE"] * 1024 / 1e6:.1f} MB)')
+    raw = (vals['FETCH_SIZE'] + vals['WRITE_SIZE']) * 1024
+    a.traffic_raw = raw
+    return hbm, (f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over {kname} dispatches '
+                 f'{TRAFFIC_SKIP}..{TRAFFIC_FRAMES - 1} of the bench ' + ('decoders' if kname == 'dec_recon_kernel' else 'encoder') + '; bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 '
+                 f'(read {2 * vals["FETCH_SIZE"] * 1024 / 1e6:.1f} MB, written {vals["WRITE_SIZE"] * 1024 / 1e6:.1f} MB). '
+                 f'The doubling is the guide\'s gfx950 correction for wide streaming reads; this kernel also does narrow '
+                 f'loads, so 2 x FETCH_SIZE is an upper bound on its reads and the raw counters ({raw / 1e6:.1f} MB) a lower bound')
 
 
-def gpu_parity(a, oracle_hashes, i_only=False):
-    """Stream 0's first frames on the GPU (fresh encoder + decoder, the bench's geometry and bitrate)
+def oracle_hashes(a, mode, sid):
+    """the oracle's sha256 of synthetic stream sid's first frames (N > 1 ranks; child process, no GPU)"""
+    cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
+           '--bitrate', str(a.bitrate), '--mode', mode, '--hash', str(a.parity_frames), '--hash-stream', str(sid), '--hash-only']
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        return json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])['parity_hashes']
+    except Exception:
+        return []  # reported as a failed parity check (no hashes)
+
+
+def gpu_parity(a, oracle_hashes, i_only=False, sid=0):
+    """Stream sid's first frames on the GPU (fresh encoder + decoder, the bench's geometry and bitrate)
     vs the oracle's sha256 of the same frames: NAL bytes and decoded pictures."""
     import numpy as np
     import torch
@@ -173,7 +207,7 @@ def gpu_parity(a, oracle_hashes, i_only=False):
     from h264mi.synth import SyntheticStream
     if not oracle_hashes:
         return False, 'no oracle hashes (CPU baseline leg failed or skipped)'
-    g = SyntheticStream(0, a.width, a.height)
+    g = SyntheticStream(sid, a.width, a.height)
     enc = h264mi.BatchEncoder(a.width, a.height, a.bitrate, 1)
     enc.set_frame_skip(False)  # as the timed encoder (see bench_encode)
     dec = h264mi.BatchDecoder(a.width, a.height, 1)
@@ -191,7 +225,7 @@ def gpu_parity(a, oracle_hashes, i_only=False):
         ok = ok and hashlib.sha256(nal).hexdigest() == want['nal'] and hashlib.sha256(pic).hexdigest() == want['pic']
     enc.close()
     dec.close()
-    return ok, f'stream 0 frames 0..{len(oracle_hashes) - 1}: ' + ('pass' if ok else 'FAIL')
+    return ok, f'stream {sid} frames 0..{len(oracle_hashes) - 1}: ' + ('pass' if ok else 'FAIL')
 
 
 def timed(run_steps, K, W, dist, sync):
@@ -221,12 +255,17 @@ def main():
     if a.traffic_probe:
         return traffic_probe(a)
     mode = {2: 'enc_i', 4: 'dec'}.get(a.config, 'encdec')
-    # CPU baseline + oracle parity hashes first, in child processes, before this process touches the GPU
-    cpu = None
+    # CPU baseline + oracle parity hashes first, in child processes, before this process touches the GPU.
+    # At N > 1 every rank takes the oracle's hashes of its own first stream (no timing).
+    cpu, hashes = None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, mode)
-    a.traffic_measured = (None, 'not measured (--no-traffic, decode-only config or N > 1)')
-    if rank == 0 and world == 1 and not a.no_traffic and a.config != 4:
+        hashes = cpu.get('parity_hashes')
+    elif world > 1 and not a.no_cpu_baseline:
+        hashes = oracle_hashes(a, mode, rank * a.streams)
+    a.traffic_kernel = 'dec_recon_kernel' if a.config == 4 else 'enc_mb_kernel'
+    a.traffic_measured = (None, 'not measured (--no-traffic or N > 1)')
+    if rank == 0 and world == 1 and not a.no_traffic:
         a.traffic_measured = measure_traffic(a)
     import numpy as np
     import torch
@@ -249,10 +288,13 @@ def main():
     else:
         res = bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank)
     # the oracle parity check runs after the timed region: its own encoder and decoder (and their HIP
-    # streams) would otherwise exist before the timed pipeline's streams are created
-    parity_ok, parity_msg = True, 'skipped (--no-cpu-baseline or N > 1)'
-    if cpu is not None:
-        parity_ok, parity_msg = gpu_parity(a, cpu.get('parity_hashes'), i_only=a.config == 2)
+    # streams) would otherwise exist before the timed pipeline's streams are created. At N > 1 each rank
+    # checks its own first stream.
+    parity_ok, parity_msg = True, 'skipped (--no-cpu-baseline)'
+    if hashes is not None:
+        parity_ok, parity_msg = gpu_parity(a, hashes, i_only=a.config == 2, sid=rank * a.streams)
+        if world > 1:
+            parity_msg = f'rank {rank} (stream {rank * a.streams}) ' + parity_msg
     parity_ok = parity_ok and res.pop('selfcheck_ok')
     elapsed = res.pop('elapsed')
     if dist:
@@ -262,11 +304,14 @@ def main():
         ok = torch.tensor([1 if parity_ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity_ok = bool(ok.item())
+        if hashes is not None:
+            parity_msg = f'all {world} ranks, each its first stream vs the oracle: ' + ('pass' if parity_ok else 'FAIL')
     frames = res.pop('frames_per_rank') * world
     value = frames / elapsed
     if rank == 0:
         if cpu is not None:
-            cpu = {k: cpu.get(k) for k in ('value', 'unit', 'cores', 'kind', 'sample', 'value_1core')}
+            cpu = {k: cpu.get(k) for k in ('value', 'unit', 'cores', 'kind', 'sample', 'value_1core', 'build', 'encode_only')
+                   if k in cpu}
         out = {
             'metric': METRIC + ' (parity vs oracle; OpenH264 parity unpinned)',
             'value': value if parity_ok else None, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
@@ -288,10 +333,12 @@ def main():
 def roofline(kernel, alg_bytes, ms_total, launches, a, note=None):
     kavg = ms_total / max(launches, 1)
     achieved = alg_bytes / (kavg / 1e3) / 1e9 if kavg > 0 else 0.0
-    traffic, tnote = a.traffic_measured if kernel == 'enc_mb_kernel' else (None, 'no PMC pass for this kernel')
+    traffic, tnote = a.traffic_measured if kernel == a.traffic_kernel else (None, 'no PMC pass for this kernel')
+    raw = getattr(a, 'traffic_raw', None) if traffic else None
     r = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic, 'alg_bytes_per_launch': alg_bytes, 'avg_launch_ms': kavg,
          'launches': launches, 'traffic_note': tnote,
+         'traffic_range': [raw, traffic] if traffic else None,
          'traffic_x_alg': traffic / alg_bytes if traffic else None}
     if note:
         r['note'] = note
@@ -334,6 +381,9 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     ev_enc = [torch.cuda.Event() for _ in range(NB)]
     ev_dec = [torch.cuda.Event() for _ in range(NB)]
     gather = NalGather(dist, torch, S, slot, G, rank, world, dev) if world > 1 else None
+    # the size all-gather and the sends of a group are ordered after the encoder's staging of that group
+    # only (a stream of their own), never after its decode: NalGather's host reads are one group late
+    gs = torch.cuda.Stream(device=dev) if gather is not None else None
     state = {'t': 0, 'g': 0}
 
     def run_group(n):
@@ -357,9 +407,11 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                 ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
                 szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
                 dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])
-            if gather is not None:
-                gather.submit(stage[b], stage_sz[b], n, b)  # sizes gathered once per group; sends of the previous group
             ev_dec[b].record(ds)
+        if gather is not None:
+            with torch.cuda.stream(gs):
+                gs.wait_event(ev_enc[b])
+                gather.submit(stage[b], stage_sz[b], n, b)  # sizes gathered once per group; sends of the previous group
         state['g'] += 1
 
     def run_steps(k):
@@ -389,17 +441,39 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     elapsed = timed(run_steps, a.steps, 0, dist, sync)
     ems, en = enc.kernel_time()
     kern = {'enc_mb_kernel': {'avg_ms': ems / max(en, 1), 'launches': en}}
+    gather_check = None
+    if gather is not None:  # the last group's units as rank 0 received them == what every rank staged
+        sync()
+        b = (state['g'] - 1) % NB
+        n = len(gather.received[-1]) // (world * S)
+        szs = stage_sz[b][:n].cpu().reshape(-1).tolist()
+        host = stage[b][:n].reshape(-1).cpu()
+        mine = [hashlib.sha256(bytes(host[u * slot:u * slot + szs[u]].numpy())).hexdigest() for u in range(n * S)]
+        allh = [None] * world
+        dist.all_gather_object(allh, mine)
+        if rank == 0:
+            rx = gather.rx[:world * n * S * slot].cpu()
+            sz = gather.received[-1]
+            got = [hashlib.sha256(bytes(rx[u * slot:u * slot + sz[u]].numpy())).hexdigest() for u in range(world * n * S)]
+            gather_check = got == [h for r in range(world) for h in allh[r]]
+        gather_check = {'ok': gather_check, 'units': world * n * S, 'host_waits': gather.host_waits}
     if decode:
         rms, rn = dec.kernel_time(0)
         pms, pn = dec.kernel_time(1)
         kern['dec_recon_kernel'] = {'avg_ms': rms / max(rn, 1), 'launches': rn}
         kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': S * G}
         if os.environ.get('H264MI_PARSE_PROF'):  # diagnostic: the slices' own duration (wave start to end)
-            nsl = S * G * max(2, min(8, 32 // G))
+            nsl = S * G * dec.ring_groups()
             prof = np.zeros(nsl * 16, np.uint64)
             h264mi.lib().h264mi_dec_parse_profile(dec._d, prof.ctypes.data)
             kern['dec_parse_kernel']['slice_ms_mean_all_calls'] = float(prof.reshape(-1, 16)[:, 0].sum()) / 1e5 / max(1, (a.warmup + a.steps) * S)
     sizes = enc.nal_sizes()
+    enc.close()
+    if dec is not None:
+        dec.close()
+    if a.parse_cus > 0:
+        h264mi.destroy_stream(es)
+        h264mi.destroy_stream(ds)
     # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
     # (read source F + read reference F + write reconstruction F) for a P frame, 2F for an IDR
     # 
@@ -412,8 +486,11 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'parse_streams': a.parse_streams,
            'parallelism': f'streams x{world} (weak)'}
+    if gather_check is not None:
+        selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
     return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg,
             'roofline': roofline('enc_mb_kernel', alg, ems, en, a), 'kernels': kern,
+            'nal_gather': gather_check,
             'selfcheck_ok': selfcheck_ok,
             'selfcheck': ('decoder output == encoder reconstruction for every stream: ' + ('pass' if selfcheck_ok else 'FAIL'))
             if decode else 'n/a (encode only)',
@@ -469,6 +546,10 @@ def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
     elapsed = timed(run_steps, a.steps, 0, None, sync)
     rms, rn = dec.kernel_time(0)
     pms, pn = dec.kernel_time(1)
+    dec.close()
+    enc.close()
+    if a.parse_cus > 0:
+        h264mi.destroy_stream(ds)
     alg = S * 2 * F  # decode P: read reference F + write picture F, per stream
     cfg = {'workload': f'{W}x{H} decode only: {S} concurrent decoders of one IPPP stream ({a.bitrate} bps, '
                        f'{sum(nbytes) // n} B/frame mean), decode batches of {G} frames',

@@ -86,6 +86,9 @@ int h264mi_enc_encode(h264mi_encoder *e, const void *d_frames);     /* async; ns
 /* rate-control frame skipping (on by default, as the wrapper's OpenH264): a skipped frame has 0 NAL bytes */
 int h264mi_enc_set_frame_skip(h264mi_encoder *e, int enable);
 int h264mi_enc_frames_skipped(h264mi_encoder *e, int stream);
+/* test hook: the next coded frame of stream fails as if its kernels had reported error code (> 0): it
+   publishes 0 NAL bytes and the frame after it is an IDR */
+int h264mi_enc_inject_error(h264mi_encoder *e, int stream, int code);
 int h264mi_enc_sync(h264mi_encoder *e);
 int h264mi_enc_nal_bytes(h264mi_encoder *e, int *out_bytes);        /* sync; -2 if a kernel reported an error */
 const void *h264mi_enc_nal_ptr(h264mi_encoder *e, int stream);     /* Annex-B bytes of the last frame (device) */
@@ -106,7 +109,16 @@ h264mi_decoder *h264mi_dec_create(int width, int height, int nstreams, void *hip
    are entropy-decoded concurrently (CAVLC parsing of a frame does not depend on other frames), then
    reconstructed in order; after the call each stream's picture is that of its last frame. */
 h264mi_decoder *h264mi_dec_create_batch(int width, int height, int nstreams, int max_frames, void *hip_stream);
+/* as h264mi_dec_create_batch with an explicit ring: groups slot groups of max_frames slots (2..16;
+   0 = the default, up to 16) and parse_streams entropy-decoding streams (1..16). A caller that waits for
+   every call (nothing to overlap) wants groups 2 and parse_streams 1: the C-ABI decoders use that. */
+h264mi_decoder *h264mi_dec_create_ring(int width, int height, int nstreams, int max_frames, int groups, int parse_streams,
+                                       void *hip_stream);
+/* device memory held by a decoder (bytes), and by a C-ABI decoder slot of an instance (0: none yet) */
+size_t h264mi_dec_device_bytes(h264mi_decoder *d);
+size_t h264mi_i_decoder_device_bytes(h264mi_instance *inst, int decoder_index);
 int h264mi_dec_max_frames(h264mi_decoder *d);
+int h264mi_dec_ring_groups(h264mi_decoder *d);  /* slot groups in the decoder's ring */
 /* number of HIP streams the entropy decoding of consecutive calls rotates over (default 3, 1..16):
    up to that many calls are entropy-decoded concurrently; synchronises the decoder */
 int h264mi_dec_set_parse_streams(h264mi_decoder *d, int nstreams);
@@ -135,12 +147,19 @@ int h264mi_dec_decode_frames_after(h264mi_decoder *d, int nframes, const void *c
    ordered after every one of the nevents hipEvent_t's; nevents 0 = h264mi_dec_decode_frames */
 int h264mi_dec_decode_frames_after_n(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
                                      const int *const *d_sizes, void *const *ready_events, int nevents);
+/* as above, and every frame's picture out: d_out[f * nstreams + s] (device, or NULL) receives frame f's
+   cropped tight I420 picture (width x height x 3/2 bytes) once it is reconstructed, d_got[...] (device
+   int, or NULL) 1 if that frame produced a picture, else 0 (the buffer is then left untouched) */
+int h264mi_dec_decode_frames_out(h264mi_decoder *d, int nframes, const void *const *d_nal, const int *nal_bytes,
+                                 const int *const *d_sizes, void *const *ready_events, int nevents, void *const *d_out,
+                                 int *const *d_got);
 int h264mi_dec_sync(h264mi_decoder *d);
 /* HIP-event timing of the decoder's kernels (bench.py): which 0 = dec_recon_kernel, 1 = dec_parse_kernel */
 int h264mi_dec_set_timing(h264mi_decoder *d, int enable);
 int h264mi_dec_kernel_time(h264mi_decoder *d, int which, double *ms_total, int *launches);
 int h264mi_dec_status(h264mi_decoder *d, int *got_pic);             /* sync; per-stream 1 = picture out */
-/* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream) (env H264MI_PARSE_PROF=1) */
+/* diagnostics: parse-kernel cycle counters, 16 per (frame slot, stream): ring_groups x max_frames x nstreams
+   slots (env H264MI_PARSE_PROF=1) */
 int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);
 /* diagnostics: the padded motion-search reference planes of a stream (luma G, b, h, j then Cb, Cr;
    sizes (cw+80)(ch+64) and (cw/2+40)(ch/2+32)), built from the last coded frame */

@@ -65,7 +65,7 @@ struct EncState {
     int32_t cur_skip;      // 1 if the frame being coded is skipped by the rate control (0 bytes out)
     int32_t skip_en;       // frame skipping enabled (the wrapper's default)
     int32_t skipped;       // frames skipped so far
-    int32_t pad_s;
+    int32_t inject_err;    // test hook (h264mi_enc_inject_error): the next coded frame fails with this code
     int32_t sps_bytes, pps_bytes;
     uint8_t sps[64], pps[32];
 };
@@ -144,7 +144,9 @@ struct DecFrame {          // per (frame slot, stream): written by dec_scan_kern
     DecParams ps;          // parameter sets in effect for this frame's slice (cropping for the output)
     NalEnt e[H264MI_MAX_NALS];
 };
-struct DecInput { const uint8_t *nal; const int32_t *size_dev; int32_t size, pad; };  // one access unit
+// one access unit; out / got (optional, device): where dec_output_kernel puts this frame's cropped tight
+// I420 picture and its got-picture flag once the frame is reconstructed (every frame of a batched call)
+struct DecInput { const uint8_t *nal; const int32_t *size_dev; int32_t size, pad; uint8_t *out; int32_t *got; };
 
 struct DecDesc {
     uint8_t *cur[3];        // unfiltered reconstruction (coded size)

@@ -5,15 +5,16 @@
 // sized from the first SPS seen in the caller's access unit. Only pic_width/height_in_mbs are read
 // here; the full SPS/PPS/slice parse runs on the GPU (dec_parse.inc). The input is untrusted caller
 // memory: every read is bounds-checked, the Exp-Golomb reader saturates instead of overflowing, and a
-// geometry outside 1..H264MI_MAX_MBS macroblocks per side is rejected (the oracle decoder applies the
-// same bound, oracle/h264o_dec.c parse_sps).
+// geometry outside 1..H264MI_MAX_MBS macroblocks per side is rejected.
 #pragma once
 #include <cstdint>
 #include <vector>
 
 namespace h264mi {
 
-constexpr int H264MI_MAX_MBS = 1024;  // per side: 16384 luma samples
+// per side: 4096 luma samples. The one limit for the peek and the decoder's allocation (dec_create):
+// an SPS the peek accepts is one the decoder can be created for.
+constexpr int H264MI_MAX_MBS = 256;
 
 inline bool host_peek_sps(const uint8_t *d, int n, int *mbw, int *mbh) {
     if (!d || n <= 0) return false;

@@ -11,8 +11,11 @@ Layering:
 
 There is no CPU fallback: importing this module on a machine without the built library raises.
 """
+import atexit
 import ctypes
 import os
+import sys
+import weakref
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('H264MI_LIB') or os.path.join(os.path.dirname(_HERE), 'lib', 'libh264mi.so')  # env: diagnostics
@@ -44,6 +47,7 @@ def lib():
             'h264mi_enc_encode': (i, [vp, vp]),
             'h264mi_enc_set_frame_skip': (i, [vp, i]),
             'h264mi_enc_frames_skipped': (i, [vp, i]),
+            'h264mi_enc_inject_error': (i, [vp, i, i]),
             'h264mi_enc_sync': (i, [vp]),
             'h264mi_enc_nal_bytes': (i, [vp, vp]),
             'h264mi_enc_nal_ptr': (vp, [vp, i]),
@@ -62,9 +66,16 @@ def lib():
             'h264mi_dec_create': (vp, [i, i, i, vp]),
             'h264mi_dec_destroy': (None, [vp]),
             'h264mi_dec_create_batch': (vp, [i, i, i, i, vp]),
+            'h264mi_dec_create_ring': (vp, [i, i, i, i, i, i, vp]),
+            'h264mi_dec_device_bytes': (ctypes.c_size_t, [vp]),
+            'h264mi_dec_ring_groups': (i, [vp]),
+            'h264mi_i_decoder_device_bytes': (ctypes.c_size_t, [vp, i]),
+            'h264mi_instance_create': (vp, []),
+            'h264mi_instance_destroy': (None, [vp]),
             'h264mi_dec_decode_frames': (i, [vp, i, vp, vp, vp]),
             'h264mi_dec_decode_frames_after': (i, [vp, i, vp, vp, vp, vp]),
             'h264mi_dec_decode_frames_after_n': (i, [vp, i, vp, vp, vp, vp, i]),
+            'h264mi_dec_decode_frames_out': (i, [vp, i, vp, vp, vp, vp, i, vp, vp]),
             'h264mi_dec_recon_profile': (i, [vp, vp]),
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_set_parse_streams': (i, [vp, i]),
@@ -98,6 +109,37 @@ def lib():
             f.argtypes = args
         _lib = L
     return _lib
+
+
+# Teardown order. GPU objects (encoders, decoders, rings, CU-masked streams) are released explicitly by
+# close(), or at interpreter exit by the atexit hook below -- which runs before the HIP runtime and torch
+# unload. __del__ does nothing once the interpreter is finalising: freeing device memory or destroying
+# streams and events from a finaliser that runs during library unload is what crashed profiled runs at
+# exit (rocprofv3 logs: SIGSEGV in __cxa_finalize).
+_live = weakref.WeakSet()
+_streams = []  # handles from h264mi_stream_create_cus not yet destroyed
+
+
+def _close_all():
+    for o in list(_live):
+        try:
+            o.close()
+        except Exception:
+            pass
+    while _streams:
+        h = _streams.pop()
+        try:
+            _hiprt().hipStreamSynchronize(ctypes.c_void_p(h))
+            lib().h264mi_stream_destroy(ctypes.c_void_p(h))
+        except Exception:
+            pass
+
+
+atexit.register(_close_all)
+
+
+def _finalising():
+    return sys.is_finalizing()
 
 
 EXPORTED = ('init_encoder', 'force_key_frame', 'init_decoder', 'deinit_decoder', 'encode_frame',
@@ -203,6 +245,7 @@ class BatchEncoder:
         self._e = self._L.h264mi_enc_create(width, height, bitrate, nstreams, ctypes.c_void_p(hs))
         if not self._e:
             raise RuntimeError('h264mi_enc_create failed')
+        _live.add(self)
 
     def encode(self, frames):
         """frames: uint8 CUDA tensor holding S tight I420 frames back to back (async)."""
@@ -217,6 +260,11 @@ class BatchEncoder:
         """rate-control frame skipping (on by default, as the wrapper's encoder)"""
         if self._L.h264mi_enc_set_frame_skip(self._e, 1 if on else 0) != 0:
             raise RuntimeError('h264mi_enc_set_frame_skip failed')
+
+    def inject_error(self, s=0, code=2):
+        """test hook: stream s's next coded frame fails (0 bytes out, then an IDR)"""
+        if self._L.h264mi_enc_inject_error(self._e, s, code) != 0:
+            raise RuntimeError('h264mi_enc_inject_error failed')
 
     def frames_skipped(self, s=0):
         return self._L.h264mi_enc_frames_skipped(self._e, s)
@@ -272,6 +320,8 @@ class BatchEncoder:
             self._e = None
 
     def __del__(self):
+        if _finalising():
+            return
         try:
             self.close()
         except Exception:
@@ -285,21 +335,34 @@ def masked_stream(cu_lo, cu_hi, complement=False):
     h = lib().h264mi_stream_create_cus(cu_lo, cu_hi, 1 if complement else 0)
     if not h:
         raise RuntimeError('h264mi_stream_create_cus failed')
+    _streams.append(h)
     return torch.cuda.ExternalStream(h)
+
+
+def destroy_stream(st):
+    """Synchronise and destroy a stream made by masked_stream() (close its users first)."""
+    h = st.cuda_stream
+    if h in _streams:
+        _streams.remove(h)
+        st.synchronize()
+        lib().h264mi_stream_destroy(ctypes.c_void_p(h))
 
 
 class BatchDecoder:
     """S independent decoder streams of one geometry; NAL units in HBM. max_frames > 1 enables
     decode_frames(): several access units per stream per call, entropy-decoded concurrently."""
 
-    def __init__(self, width, height, nstreams, stream=None, max_frames=1):
+    def __init__(self, width, height, nstreams, stream=None, max_frames=1, groups=0, parse_streams=3):
+        """groups: slot groups of max_frames frames in the decoder's ring (0 = default, up to 16; 2 for a
+        caller that waits for every call); parse_streams: HIP streams entropy decoding rotates over"""
         import torch
         self.w, self.h, self.S, self.B = width, height, nstreams, max_frames
         self._L = lib()
         hs = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        self._d = self._L.h264mi_dec_create_batch(width, height, nstreams, max_frames, ctypes.c_void_p(hs))
+        self._d = self._L.h264mi_dec_create_ring(width, height, nstreams, max_frames, groups, parse_streams, ctypes.c_void_p(hs))
         if not self._d:
             raise RuntimeError('h264mi_dec_create failed')
+        _live.add(self)
         cw, ch = ctypes.c_int(), ctypes.c_int()
         self._L.h264mi_dec_coded_size(self._d, ctypes.byref(cw), ctypes.byref(ch))
         self.cw, self.ch = cw.value, ch.value
@@ -318,11 +381,12 @@ class BatchDecoder:
         if self._L.h264mi_dec_decode_dev(self._d, ptrs, sz) != 0:
             raise RuntimeError('h264mi_dec_decode_dev failed')
 
-    def decode_frames(self, nal_ptrs, nal_sizes=None, size_ptrs=None, ready_event=None):
+    def decode_frames(self, nal_ptrs, nal_sizes=None, size_ptrs=None, ready_event=None, out_ptrs=None, got_ptrs=None):
         """async; n frames per stream: nal_ptrs[f * S + s] (device addresses), sizes either host ints
         (nal_sizes) or device int32 addresses (size_ptrs). n <= max_frames. Inputs are ordered after
         the decoder's stream, or, if ready_event (a torch.cuda.Event recorded by the producer, or a
-        list of them, one per producer stream) is given, after those events only."""
+        list of them, one per producer stream) is given, after those events only. out_ptrs / got_ptrs
+        (device addresses, same indexing): every frame's cropped tight I420 picture and got flag."""
         m = len(nal_ptrs)
         assert m % self.S == 0 and m // self.S <= self.B
         ptrs = (ctypes.c_void_p * m)(*nal_ptrs)
@@ -330,7 +394,9 @@ class BatchDecoder:
         sp = (ctypes.c_void_p * m)(*size_ptrs) if size_ptrs is not None else None
         evs = [] if ready_event is None else (list(ready_event) if isinstance(ready_event, (list, tuple)) else [ready_event])
         ev = (ctypes.c_void_p * max(1, len(evs)))(*[e.cuda_event for e in evs])
-        if self._L.h264mi_dec_decode_frames_after_n(self._d, m // self.S, ptrs, sizes, sp, ev, len(evs)) != 0:
+        op = (ctypes.c_void_p * m)(*out_ptrs) if out_ptrs is not None else None
+        gp = (ctypes.c_void_p * m)(*got_ptrs) if got_ptrs is not None else None
+        if self._L.h264mi_dec_decode_frames_out(self._d, m // self.S, ptrs, sizes, sp, ev, len(evs), op, gp) != 0:
             raise RuntimeError('h264mi_dec_decode_frames failed')
 
     def set_parse_cus(self, lo, hi):
@@ -351,6 +417,12 @@ class BatchDecoder:
         if self._L.h264mi_dec_kernel_time(self._d, which, ctypes.byref(ms), ctypes.byref(n)) != 0:
             raise RuntimeError('h264mi_dec_kernel_time failed')
         return ms.value, n.value
+
+    def device_bytes(self):
+        return self._L.h264mi_dec_device_bytes(self._d)
+
+    def ring_groups(self):
+        return self._L.h264mi_dec_ring_groups(self._d)
 
     def status(self):
         got = (ctypes.c_int * self.S)()
@@ -379,6 +451,8 @@ class BatchDecoder:
             self._d = None
 
     def __del__(self):
+        if _finalising():
+            return
         try:
             self.close()
         except Exception:
@@ -397,6 +471,7 @@ class NalRing:
         self._r = self._L.h264mi_ring_create(slots, slot_bytes)
         if not self._r:
             raise RuntimeError('h264mi_ring_create failed')
+        _live.add(self)
 
     def publish(self, enc, stream, consumers):
         t = self._L.h264mi_ring_publish(self._r, enc._e, stream, consumers)
@@ -429,6 +504,8 @@ class NalRing:
             self._r = None
 
     def __del__(self):
+        if _finalising():
+            return
         try:
             self.close()
         except Exception:
@@ -453,6 +530,8 @@ def _hiprt():
     if _hip is None:
         _hip = ctypes.CDLL('libamdhip64.so')
         _hip.hipMemcpy.restype = ctypes.c_int
+        _hip.hipStreamSynchronize.restype = ctypes.c_int
+        _hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
     return _hip
 
 

@@ -50,20 +50,27 @@ def _post(dist, buf, sz, S, n, slot, rank, world, rx, wait):
 
 
 class NalGather:
-    """Pipelined NAL gather for bench.py: one size all-gather per GROUP of n frames (not per frame),
-    and the exact-size sends of group g posted while group g+1 is being encoded, so the host never
-    waits on the group the GPU is working on. Call submit() on the decoder's stream after a group's
-    units are staged, flush() at the end; done_event(b) is recorded once group g's sends (staging
-    buffer b) are complete: the encoder waits on it before reusing the buffer."""
+    """Pipelined NAL gather for bench.py: one size all-gather per GROUP of n frames (not per frame), and
+    the exact-size sends of group g posted when group g+1 is submitted, so the host never waits on the
+    group it has just submitted.
+
+    On CUDA, call submit() on a stream that is ordered after the group's staging only (bench.py: a
+    gather stream that waits for the encoder's staging event), never after the decoder: the collective
+    then depends on nothing but the encoder. The gathered byte counts are copied into pinned host memory
+    on a side stream behind the collective (non-blocking) with an event; the host reads them one group
+    later, when that event has long completed. done_event(b) is recorded once the sends of staging
+    buffer b are complete: the encoder waits on it before reusing the buffer. flush() at the end."""
 
     def __init__(self, dist, torch, S, slot, G, rank, world, device):
         self.dist, self.torch, self.S, self.slot, self.G = dist, torch, S, slot, G
         self.rank, self.world = rank, world
         self.rx = torch.empty(world * G * S * slot, dtype=torch.uint8, device=device) if rank == 0 else None
         self.cuda = device is not None and torch.device(device).type == 'cuda'
-        self.pending = None  # (buf, gathered sizes, work, n, buffer id)
+        self.side = torch.cuda.Stream(device=device) if self.cuda else None
+        self.pending = None  # (buf, host sizes, ready event, n, buffer id)
         self.events = {}
         self.received = []   # per group: world*n*S byte counts (host), for tests / accounting
+        self.host_waits = 0  # times _finish found the earlier group's sizes not yet on the host (diagnostic)
 
     def done_event(self, b):
         return self.events.get(b)
@@ -72,9 +79,24 @@ class NalGather:
         """buf: (G, S*slot) uint8 staging tensor, sizes: (G, S) int32 byte counts; frames 0..n-1 valid"""
         t = self.torch
         flat = sizes[:n].reshape(-1).contiguous()
+        m = flat.numel()
         parts = [t.empty_like(flat) for _ in range(self.world)]
         work = self.dist.all_gather(parts, flat, async_op=True)
-        prev, self.pending = self.pending, (buf, parts, work, n, b)
+        if self.cuda:
+            host = t.empty(self.world * m, dtype=flat.dtype, pin_memory=True)
+            self.side.wait_stream(t.cuda.current_stream())
+            with t.cuda.stream(self.side):
+                work.wait()  # device-side: the side stream waits for the collective, the host does not
+                for r, q in enumerate(parts):
+                    host[r * m:(r + 1) * m].copy_(q, non_blocking=True)
+                ready = t.cuda.Event()
+                ready.record(self.side)
+            for q in parts:
+                q.record_stream(self.side)
+            pend = (buf, host, ready, n, b)
+        else:
+            pend = (buf, (parts, work), None, n, b)
+        prev, self.pending = self.pending, pend
         if prev is not None:
             self._finish(prev)
 
@@ -84,9 +106,16 @@ class NalGather:
             self._finish(p)
 
     def _finish(self, p):
-        buf, parts, work, n, b = p
-        work.wait()
-        sz = self.torch.cat(parts).cpu().tolist()  # host sync on an EARLIER group's sizes only
+        buf, host, ready, n, b = p
+        if ready is not None:
+            if not ready.query():
+                self.host_waits += 1
+            ready.synchronize()  # an EARLIER group's gathered sizes (normally complete already)
+            sz = host.tolist()
+        else:
+            parts, work = host
+            work.wait()
+            sz = self.torch.cat(parts).tolist()
         reqs = _post(self.dist, buf.reshape(-1), sz, self.S, n, self.slot, self.rank, self.world, self.rx, wait=False)
         for q in reqs:
             q.wait()  # on CUDA: orders the current stream after the transfers (no host block)

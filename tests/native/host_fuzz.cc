@@ -47,6 +47,12 @@ static void fuzz_sps() {
             std::free(p);
         }
     }
+    {  // wider than the decoder supports: the peek must refuse it (the C-ABI keeps its working decoder)
+        uint8_t sps[128];
+        const int n = (int)h264o_write_sps(16 * (h264mi::H264MI_MAX_MBS + 1), 64, sps);
+        int w = 0, h = 0;
+        CHECK(!h264mi::host_peek_sps(sps, n, &w, &h), "SPS of %d MBs per side accepted", h264mi::H264MI_MAX_MBS + 1);
+    }
     for (int t = 0; t < 20000; t++) {  // random buffers with start codes sprinkled in
         const size_t len = rnd() % 300;
         uint8_t *p = (uint8_t *)std::malloc(len ? len : 1);

@@ -1,0 +1,172 @@
+"""GPU: BASELINE.json configs at their stated spans and both bitrates (configs 2 and 3
+"1 Mbps and 8 Mbps"; the glue's own bitrate is 1 Mbps, scripts/encoder_worker.js:96), frame by frame
+against the oracle through the C-ABI the reference's glue binds (init_encoder / force_key_frame /
+encode_frame_yuv_i420 / init_decoder / decode_frame_yuv_i420, openh264_wrapper.cpp:198-464), plus the
+config-4 fan-out with EVERY frame's picture checked (batched calls carry 4 frames).
+
+Parity is with the oracle (the CPU restatement); OpenH264 parity is unpinned."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _enc(L, f, w, h):
+    p = ctypes.POINTER(ctypes.c_ubyte)()
+    sz = ctypes.c_int(0)
+    L.encode_frame_yuv_i420(f.ctypes.data, w, h, ctypes.byref(p), ctypes.byref(sz))
+    return ctypes.string_at(p, sz.value) if sz.value > 0 else b''
+
+
+def _dec(L, idx, nal, w, h, out):
+    a = np.frombuffer(nal, np.uint8).copy()
+    gw, gh = ctypes.c_int(-1), ctypes.c_int(-1)
+    L.decode_frame_yuv_i420(idx, a.ctypes.data, len(nal), out.ctypes.data, ctypes.byref(gw), ctypes.byref(gh))
+    return gw.value, gh.value
+
+
+def _run_capi(L, oracle, w, h, br, nf, i_only, sid=0):
+    """encode nf frames through the C-ABI and the oracle (same synthetic input), decode every coded
+    frame through the C-ABI decoder and the oracle decoder; returns (sizes, qps)"""
+    from h264mi.synth import SyntheticStream
+    g = SyntheticStream(sid, w, h)
+    assert L.init_encoder(w, h, br) == 0
+    assert L.init_decoder(0) == 0
+    oe, od = oracle.encoder(w, h, br), oracle.decoder()
+    out = np.zeros(w * h * 3 // 2, np.uint8)
+    sizes, qps = [], []
+    for t in range(nf):
+        f = np.ascontiguousarray(g.frame(t))
+        if i_only:
+            L.force_key_frame()
+            oe.force_idr()
+        got, ref = _enc(L, f, w, h), oe.encode(f)
+        assert got == ref, f'{w}x{h} {br} bps frame {t}: GPU {len(got)} B vs oracle {len(ref)} B'
+        sizes.append(len(ref))
+        qps.append(oe.last_qp())
+        if not ref:
+            continue
+        rc, pic, ow, oh = od.decode(ref)
+        assert rc == 1
+        gw, gh = _dec(L, 0, got, w, h, out)
+        assert (gw, gh) == (ow, oh) == (w, h), f'frame {t}: decoded {gw}x{gh}'
+        assert np.array_equal(out, pic), f'{w}x{h} {br} bps frame {t}: GPU picture != oracle picture'
+    L.deinit_decoder(0)
+    return sizes, qps
+
+
+def test_config3_1080p_ippp_8mbps_30_frames(gpu_lib, oracle):
+    """configs[2] at 8 Mbps, the non-degenerate operating point: 1 IDR + 29 P frames (frame skipping on,
+    as the wrapper's encoder), every frame coded with real residuals (QP in the 30s), NAL bytes and
+    decoded pictures == oracle frame by frame"""
+    sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 8000000, 30, False)
+    assert sum(1 for n in sizes[1:] if n > 0) >= 25, sizes  # P frames really coded
+    assert max(qps[1:]) < 45, qps                            # not the QP-51 collapse regime
+
+
+def test_config3_1080p_ippp_1mbps_rc_skipping(gpu_lib, oracle):
+    """configs[2] at the glue's 1 Mbps with the wrapper's frame skipping: the rate control drops the
+    frames its buffer cannot take (0-byte access units) -- GPU == oracle, including which
+    frames are skipped; every coded frame decodes to the oracle's picture"""
+    sizes, _ = _run_capi(gpu_lib, oracle, 1920, 1080, 1000000, 12, False)
+    assert sizes[0] > 0 and 0 in sizes[1:], sizes
+
+
+@pytest.mark.parametrize('br', [1000000, 8000000], ids=['1mbps', '8mbps'])
+def test_config2_720p_i_only_30_frames(gpu_lib, oracle, br):
+    """configs[1]: 1280x720, force_key_frame before every frame (all IDR), 30 frames, 1 and 8 Mbps"""
+    sizes, qps = _run_capi(gpu_lib, oracle, 1280, 720, br, 30, True)
+    assert all(n > 0 for n in sizes), sizes
+
+
+def test_encoder_1080p_p_frames_skip_off(gpu_lib, oracle):
+    """1080p IPPP at 1 Mbps with frame skipping off (bench.py's setting): 6 frames, all coded (P frames
+    included), batch encoder bytes == oracle bytes"""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    w, h, br = 1920, 1080, 1000000
+    g = SyntheticStream(0, w, h)
+    enc = h264mi.BatchEncoder(w, h, br, 1)
+    enc.set_frame_skip(False)
+    oe = oracle.encoder(w, h, br)
+    oe.set_frame_skip(False)
+    for t in range(6):
+        f = np.ascontiguousarray(g.frame(t))
+        enc.encode(torch.from_numpy(f).cuda())
+        n = enc.nal_sizes()[0]
+        ref = oe.encode(f)
+        assert n > 0 and enc.nal_bytes(0, n) == ref, f'frame {t}'
+    enc.close()
+
+
+def _oracle_stream(oracle, w, h, br, nf, sid=0):
+    from h264mi.synth import SyntheticStream
+    g = SyntheticStream(sid, w, h)
+    oe, od = oracle.encoder(w, h, br), oracle.decoder()
+    oe.set_frame_skip(False)
+    units, pics = [], []
+    for t in range(nf):
+        u = oe.encode(np.ascontiguousarray(g.frame(t)))
+        rc, pic, _, _ = od.decode(u)
+        assert rc == 1
+        units.append(u)
+        pics.append(hashlib.sha256(pic.tobytes()).hexdigest())
+    return units, pics
+
+
+@pytest.mark.parametrize('br', [1000000, 8000000], ids=['1mbps', '8mbps'])
+def test_config4_every_frame_8_decoders(gpu_lib, oracle, br):
+    """configs[3]: one 1080p IPPP stream decoded by 8 concurrent decoders, 4 frames per call; EVERY
+    frame's picture of every decoder (per-frame outputs of the batched call) == the oracle's picture"""
+    import torch
+    import h264mi
+    w, h, nf, S, G = 1920, 1080, 12, 8, 4
+    units, pics = _oracle_stream(oracle, w, h, br, nf)
+    dev = [torch.from_numpy(np.frombuffer(u, np.uint8).copy()).cuda() for u in units]
+    F = w * h * 3 // 2
+    out = torch.zeros((nf, S, F), dtype=torch.uint8, device='cuda')
+    got = torch.full((nf, S), -1, dtype=torch.int32, device='cuda')
+    dec = h264mi.BatchDecoder(w, h, S, max_frames=G)
+    for t0 in range(0, nf, G):
+        fr = range(t0, t0 + G)
+        dec.decode_frames([dev[t].data_ptr() for t in fr for _ in range(S)], nal_sizes=[len(units[t]) for t in fr for _ in range(S)],
+                          out_ptrs=[out[t, s].data_ptr() for t in fr for s in range(S)],
+                          got_ptrs=[got[t, s].data_ptr() for t in fr for s in range(S)])
+    rc, _ = dec.status()
+    assert rc == 0
+    assert got.cpu().eq(1).all()
+    host = out.cpu().numpy()
+    for t in range(nf):
+        for s in range(S):
+            assert hashlib.sha256(host[t, s].tobytes()).hexdigest() == pics[t], f'frame {t} decoder {s}'
+    dec.close()
+
+
+def test_capi_decoder_memory_1080p(gpu_lib, oracle):
+    """a C-ABI decoder slot (one call in flight: two slot groups, one parse stream) holds well under
+    64 MB at 1080p; a pipelined batch decoder's default ring is larger"""
+    import h264mi
+    L = gpu_lib
+    inst = L.h264mi_instance_create()
+    w, h = 1920, 1080
+    units, _ = _oracle_stream(oracle, w, h, 8000000, 1)
+    a = np.frombuffer(units[0], np.uint8).copy()
+    out = np.zeros(w * h * 3 // 2, np.uint8)
+    gw, gh = ctypes.c_int(), ctypes.c_int()
+    L.h264mi_i_init_decoder.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.h264mi_i_decode_frame_yuv_i420.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p]
+    assert L.h264mi_i_init_decoder(inst, 3) == 0
+    L.h264mi_i_decode_frame_yuv_i420(inst, 3, a.ctypes.data, len(a), out.ctypes.data, ctypes.byref(gw), ctypes.byref(gh))
+    assert (gw.value, gh.value) == (w, h)
+    capi = L.h264mi_i_decoder_device_bytes(inst, 3)
+    L.h264mi_instance_destroy(inst)
+    dec = h264mi.BatchDecoder(w, h, 1)
+    batch = dec.device_bytes()
+    dec.close()
+    assert 0 < capi < 64 << 20, capi
+    assert batch > capi, (batch, capi)

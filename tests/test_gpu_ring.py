@@ -210,3 +210,51 @@ def test_ring_wraps_without_host_sync(gpu_lib):
         d.close()
     ring.close()
     enc.close()
+
+
+def test_ring_failed_frame_publishes_nothing(gpu_lib, oracle):
+    """A frame whose kernels fail (injected as an RBSP overflow) publishes nothing to the ring -- no
+    truncated access unit reaches a consumer -- and the encoder restarts with an IDR (SPS + PPS + IDR
+    slice): the decoder, which never saw the failed frame, decodes the stream on."""
+    import torch
+    import h264mi
+    w, h, n, bad = 176, 144, 5, 2
+    frames = _frames(w, h, n, 7)
+    enc = h264mi.BatchEncoder(w, h, 300000, 1)
+    enc.set_frame_skip(False)
+    dec = h264mi.BatchDecoder(w, h, 1)
+    ring = h264mi.NalRing(slots=4, slot_bytes=1 << 18)
+    od = oracle.decoder()
+    for t in range(n):
+        if t == bad:
+            enc.inject_error(0, 2)
+        enc.encode(frames[t])
+        tk = ring.publish(enc, 0, 1)
+        torch.cuda.synchronize()
+        size = torch.empty(1, dtype=torch.int32)
+        h264mi._hip_memcpy_d2h(size.data_ptr(), ring.size_ptr(tk), 4)
+        nb = int(size[0])
+        if t == bad:
+            assert nb == 0, 'a failed frame reached the ring'
+            ring.release(tk)
+            continue
+        assert nb > 0
+        unit = torch.empty(nb, dtype=torch.uint8)
+        h264mi._hip_memcpy_d2h(unit.data_ptr(), ring.nal_ptr(tk), nb)
+        u = bytes(unit.numpy())
+        types = [u[i + 4] & 31 for i in range(len(u) - 4) if u[i:i + 4] == b'\x00\x00\x00\x01']
+        if t in (0, bad + 1):
+            assert types[:3] == [7, 8, 5], (t, types)  # the frame after the failure restarts with an IDR
+        else:
+            assert types == [1], (t, types)
+        dec.decode_frames([ring.nal_ptr(tk)], size_ptrs=[ring.size_ptr(tk)])
+        ring.release(tk)
+        rc, got = dec.status()
+        orc, opic, _, _ = od.decode(u)
+        assert rc == 0 and got == [1] and orc == 1
+        assert dec.picture_i420(0) == opic.tobytes(), f'frame {t}'
+    st = ring.stats()
+    assert st['published'] == n - 1 and st['ref_counts'] == [0] * 4
+    dec.close()
+    ring.close()
+    enc.close()

@@ -144,3 +144,49 @@ def test_stream_ids_partition():
     from h264mi.shard import stream_ids
     allids = [i for r in range(8) for i in stream_ids(r, 4)]
     assert allids == list(range(32))  # config 5: 32 streams over 8 GPUs
+
+
+class _FakeWork:
+    def __init__(self, log, g):
+        self.log, self.g = log, g
+
+    def wait(self):
+        self.log.append(self.g)
+
+
+class _FakeDist:
+    """records which group's size all-gather the host waited on (world 1: rank 0 copies its own units)"""
+    P2POp = None
+
+    def __init__(self):
+        self.log, self.calls = [], 0
+
+    def all_gather(self, parts, flat, async_op=False):
+        for p in parts:
+            p.copy_(flat)
+        w = _FakeWork(self.log, self.calls)
+        self.calls += 1
+        return w
+
+    def batch_isend_irecv(self, ops):
+        return []
+
+
+def test_submit_does_not_wait_on_current_group():
+    """NalGather.submit(group g) waits (host side) only for group g-1's size gather, never for g's own:
+    the host goes on to enqueue group g+1's encode while g is still in flight (VERDICT r2 weak #7)."""
+    from h264mi.shard import NalGather
+    fd = _FakeDist()
+    S, slot, G = 2, 16, 2
+    gat = NalGather(fd, torch, S, slot, G, 0, 1, None)
+    bufs = [torch.arange(G * S * slot, dtype=torch.int64).to(torch.uint8).reshape(G, S * slot) + k for k in range(3)]
+    sizes = torch.full((G, S), 5, dtype=torch.int32)
+    gat.submit(bufs[0], sizes, G, 0)
+    assert fd.log == []          # group 0 just submitted: nothing waited on
+    gat.submit(bufs[1], sizes, G, 1)
+    assert fd.log == [0]         # only the earlier group
+    gat.submit(bufs[2], sizes, 1, 2)
+    assert fd.log == [0, 1]
+    gat.flush()
+    assert fd.log == [0, 1, 2]
+    assert gat.received[-1] == [5] * S and torch.equal(gat.rx[:slot * S], bufs[2][0])

@@ -21,7 +21,7 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
     gens = [SyntheticStream(s, w, h) for s in range(S)]
     enc = h264mi.BatchEncoder(w, h, br, S)
     enc.set_frame_skip(False)  # every frame coded, as in bench.py
-    dec = h264mi.BatchDecoder(w, h, S)
+    dec = h264mi.BatchDecoder(w, h, S, groups=2, parse_streams=1)
     if LOAD:
         es = torch.cuda.Stream()
         lenc = h264mi.BatchEncoder(w, h, br, 8, stream=es)
@@ -30,7 +30,7 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
         lclip = [torch.from_numpy(np.concatenate([g.frame(t) for g in lgen])).cuda() for t in range(4)]
     L = h264mi.lib()
     names = ['-', '-', '-', 'ring-fill', 'skip-runs', 'mb-hdr', 'residual-rest', 'record', 'qp+ctx', 'luma', 'chromaDC', 'chromaAC']
-    NSL = S * max(2, min(8, 32 // 1))  # frame slots of a max_frames=1 decoder (runtime_dec.inc: NG groups)
+    NSL = S * dec.ring_groups()  # frame slots of a max_frames=1 decoder
     prev = np.zeros(NSL * 16, np.uint64)
     for t in range(nf):
         frames = torch.from_numpy(np.concatenate([g.frame(t) for g in gens])).cuda()
