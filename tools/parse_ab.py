@@ -7,7 +7,8 @@ import hashlib, json, os, subprocess, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
-W, H, BR = 1920, 1080, 1000000
+W, H = 1920, 1080
+BR = int(os.environ.get('PARSE_AB_BR', '1000000'))
 
 
 def encode(path, nf):
@@ -27,7 +28,7 @@ def encode(path, nf):
 def decode(path):
     import torch, h264mi
     units = list(np.load(path).values())
-    dec = h264mi.BatchDecoder(W, H, 1, max_frames=1)
+    dec = h264mi.BatchDecoder(W, H, 1, max_frames=1, groups=2, parse_streams=1)
     dev = [torch.from_numpy(u.copy()).cuda() for u in units]
     torch.cuda.synchronize()
     per, hs = [], hashlib.sha256()
