@@ -55,6 +55,8 @@ def parse():
     ap.add_argument('--group', type=int, default=0,
                     help='frames per stream per decode call (frame-parallel entropy decoding); default 4, 16 for the '
                          'decode-only config (no encoder latency to hide: more slices in flight)')
+    ap.add_argument('--no-tail-frames', dest='tail_frames', action='store_false',
+                    help='decode the last group of a run as one call too (default: frame by frame)')
     ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
     ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
     ap.add_argument('--parse-cus', type=int, default=-1,
@@ -415,9 +417,16 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         state['g'] += 1
 
     def run_steps(k):
+        # groups of G frames; the last group of a run is decoded frame by frame, so the pipeline drains
+        # at frame granularity (each of its frames is entropy-decoded as soon as it is encoded, instead of
+        # after the whole group)
         while k > 0:
             n = min(G, k)
-            run_group(n)
+            if k <= G and a.tail_frames:
+                for _ in range(n):
+                    run_group(1)
+            else:
+                run_group(n)
             k -= n
         if gather is not None:
             gather.flush()

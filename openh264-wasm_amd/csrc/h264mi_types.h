@@ -111,6 +111,7 @@ struct PlanesDesc {
 // Per-stream decoder state + buffers.
 struct DecParams {          // SPS/PPS fields the slice layer needs (7.3.2.1, 7.3.2.2)
     int32_t have_sps, have_pps, mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4];
+    int32_t dpoaz;         // delta_pic_order_always_zero_flag (POC type 1)
     int32_t nref, qp, cqp, dbkc, red, bfp;
     int32_t has_ref;       // parse-side view: a picture has been decoded before (P slices allowed)
 };

@@ -16,7 +16,7 @@
 
 struct H264ODec {
     int have_sps, have_pps;
-    int mbw, mbh, log2_mfn, poc_type, log2_poc, crop[4], frame_mbs_only;
+    int mbw, mbh, log2_mfn, poc_type, log2_poc, dpoaz, crop[4], frame_mbs_only;
     int num_ref_default, pic_init_qp, cqp_off, dbk_ctrl, constrained_intra, redundant, bottom_field_poc, weighted;
     int cw, ch;
     uint8_t *cur[3], *ref[3];
@@ -38,10 +38,10 @@ static int parse_sps(H264ODec *d, BR *r) {
     if (profile == 100 || profile == 110 || profile == 122 || profile == 244 || profile == 44 || profile == 83 ||
         profile == 86 || profile == 118 || profile == 128) return -1; /* High profiles: out of scope */
     int log2_mfn = br_ue(r) + 4;
-    int poc_type = br_ue(r), log2_poc = 0;
+    int poc_type = br_ue(r), log2_poc = 0, dpoaz = 0;
     if (poc_type == 0) log2_poc = br_ue(r) + 4;
     else if (poc_type == 1) {
-        br_get(r, 1); br_se(r); br_se(r);
+        dpoaz = br_get(r, 1); br_se(r); br_se(r);  /* delta_pic_order_always_zero_flag */
         int n = br_ue(r);
         for (int i = 0; i < n; i++) br_se(r);
     }
@@ -64,7 +64,7 @@ static int parse_sps(H264ODec *d, BR *r) {
         d->mbs = (MBInfo *)calloc((size_t)mbw * mbh, sizeof(MBInfo));
         d->has_ref = 0;
     }
-    d->log2_mfn = log2_mfn; d->poc_type = poc_type; d->log2_poc = log2_poc;
+    d->log2_mfn = log2_mfn; d->poc_type = poc_type; d->log2_poc = log2_poc; d->dpoaz = dpoaz;
     memcpy(d->crop, crop, sizeof(crop));
     d->have_sps = 1;
     return 0;
@@ -236,8 +236,10 @@ static void set_part(MBInfo *mb, int bx, int by, int pw, int ph, const int mv[2]
 }
 
 static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
-    (void)nal_ref_idc;
     if (!d->have_sps || !d->have_pps) return -1;
+    /* a non-reference picture (nal_ref_idc 0) must not become the reference of the next P slice, and
+     * carries no dec_ref_pic_marking(); the wrapper's encoder never emits one: rejected (out of scope) */
+    if (nal_ref_idc == 0) return -1;
     int first_mb = br_ue(r);
     int st = br_ue(r) % 5;           /* 0 P, 2 I */
     br_ue(r);
@@ -246,7 +248,7 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
     br_get(r, d->log2_mfn);
     if (nal_type == 5) br_ue(r);
     if (d->poc_type == 0) { br_get(r, d->log2_poc); if (d->bottom_field_poc) br_se(r); }
-    else if (d->poc_type == 1) { br_se(r); if (d->bottom_field_poc) br_se(r); }
+    else if (d->poc_type == 1 && !d->dpoaz) { br_se(r); if (d->bottom_field_poc) br_se(r); }
     if (d->redundant) br_ue(r);
     int nref = d->num_ref_default;
     if (st == 0) {

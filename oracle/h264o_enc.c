@@ -22,7 +22,9 @@
 #define QP_MAX 51
 #define LOG2_MAX_FRAME_NUM 16
 #define LOG2_MAX_POC_LSB 16
+#ifndef CROSS_THR
 #define CROSS_THR 1024  /* cross search when the best integer cost exceeds this */
+#endif
 
 struct H264OEnc {
     int w, h, mbw, mbh, cw, ch;

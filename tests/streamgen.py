@@ -133,7 +133,7 @@ def _ok(needs, top, left):
 
 
 class SyntaxGen:
-    def __init__(self, oracle_so, mbw, mbh, seed, crop_right=0, crop_bottom=0, cqp=0, init_qp=26):
+    def __init__(self, oracle_so, mbw, mbh, seed, crop_right=0, crop_bottom=0, cqp=0, init_qp=26, poc_type=0, dpoaz=0):
         import ctypes
         self.ct = ctypes
         L = ctypes.CDLL(oracle_so)
@@ -144,6 +144,7 @@ class SyntaxGen:
         self.rng = np.random.default_rng(seed)
         self.crop = (crop_right, crop_bottom)
         self.cqp, self.init_qp = cqp, init_qp
+        self.poc_type, self.dpoaz = poc_type, dpoaz  # POC type 0 / 1 (delta_pic_order_always_zero_flag) / 2
         self.frame_num = 0
         self.poc = 0
         self.idr_id = 0
@@ -154,7 +155,11 @@ class SyntaxGen:
         w = FastBits()
         w.u(66, 8); w.u(0xC0, 8); w.u(40, 8); w.ue(0)
         w.ue(12)              # log2_max_frame_num_minus4 (16 bits)
-        w.ue(0); w.ue(12)     # POC type 0, 16-bit lsb
+        w.ue(self.poc_type)
+        if self.poc_type == 0:
+            w.ue(12)          # 16-bit lsb
+        elif self.poc_type == 1:
+            w.u(self.dpoaz, 1); w.se(-1); w.se(0); w.ue(2); w.se(2); w.se(3)
         w.ue(1); w.u(0, 1)
         w.ue(self.mbw - 1); w.ue(self.mbh - 1)
         w.u(1, 1); w.u(1, 1)
@@ -305,7 +310,7 @@ class SyntaxGen:
         self._residual(w, nn, mx, my, cur, 'i16', cbpl | (cbpc << 4), qp, True)
         return qp, cur, None
 
-    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24):
+    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24, ref_idc=2):
         rng = self.rng
         mbw, mbh = self.mbw, self.mbh
         w = FastBits()
@@ -315,7 +320,10 @@ class SyntaxGen:
         w.u(self.frame_num & 0xffff, 16)
         if idr:
             w.ue(self.idr_id)
-        w.u(self.poc & 0xffff, 16)
+        if self.poc_type == 0:
+            w.u(self.poc & 0xffff, 16)
+        elif self.poc_type == 1 and not self.dpoaz:
+            w.se(int(rng.integers(-3, 4)))    # delta_pic_order_cnt[0]
         if not idr:
             w.u(1 if override else 0, 1)
             if override:
@@ -326,7 +334,7 @@ class SyntaxGen:
                 w.ue(3)
         if idr:
             w.u(0, 1); w.u(0, 1)
-        else:
+        elif ref_idc:                         # dec_ref_pic_marking() only in reference pictures
             w.u(0, 1)
         qp_delta = min(51 - self.init_qp, max(-self.init_qp, qp_delta))  # SliceQPY in 0..51
         qp = self.init_qp + qp_delta
@@ -393,13 +401,14 @@ class SyntaxGen:
         self.frame_num, self.poc = 1, 2
         return self.sps() + self.pps() + nal(3, 5, body)
 
-    def p(self, mix=None, **kw):
-        """one P picture with every macroblock type"""
+    def p(self, mix=None, ref_idc=2, **kw):
+        """one P picture with every macroblock type (ref_idc 0: a non-reference picture)"""
         mix = mix or {'skip': 3, 'p16': 3, 'p16x8': 2, 'p8x16': 2, 'p8x8': 3, 'i4': 1, 'i16': 1, 'pcm': 0.3}
-        body = self._slice(False, mix, **kw)
-        self.frame_num = (self.frame_num + 1) & 0xffff
+        body = self._slice(False, mix, ref_idc=ref_idc, **kw)
+        if ref_idc:
+            self.frame_num = (self.frame_num + 1) & 0xffff
         self.poc += 2
-        return nal(2, 1, body)
+        return nal(ref_idc, 1, body)
 
 
 _CHROMA_QP = [i for i in range(30)] + [29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39]

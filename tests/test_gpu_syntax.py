@@ -39,6 +39,27 @@ def test_full_syntax_vs_oracle(gpu_lib, oracle, case):
     L.deinit_decoder(12)
 
 
+@pytest.mark.parametrize('poc', [(1, 0), (1, 1), (2, 0)], ids=['poc1', 'poc1_always_zero', 'poc2'])
+def test_poc_types_and_non_reference_vs_oracle(gpu_lib, oracle, poc):
+    """POC types 1 and 2 (the slice header's POC fields by the SPS's rules): every picture == the
+    oracle's; a non-reference P picture (nal_ref_idc 0) is out of scope and yields no picture, as in the
+    oracle, and the stream decodes on from the last reference picture"""
+    from streamgen import SyntaxGen
+    g = SyntaxGen(SO, 11, 9, 21, poc_type=poc[0], dpoaz=poc[1])
+    units = [g.idr(), g.p(), g.p(ref_idc=0), g.p()]
+    od = oracle.decoder()
+    L = gpu_lib
+    assert L.init_decoder(14) == 0
+    for k, u in enumerate(units):
+        rc, pic, _, _ = od.decode(u)
+        gw, gh, got = gpu_decode(L, 14, u, 176, 144)
+        if k == 2:
+            assert rc != 1 and (gw, gh) == (0, 0), f'unit {k}: non-reference picture'
+            continue
+        assert rc == 1 and (gw, gh) == (176, 144) and np.array_equal(got, pic), f'unit {k}'
+    L.deinit_decoder(14)
+
+
 def test_full_syntax_1080p_vs_oracle(gpu_lib, oracle):
     """the same syntax at 1920x1080 (cropped from 1088), chroma_qp_index_offset 3: IDR + 2 P pictures,
     through the C-ABI (one frame per call) and the frame-batched decoder (both P frames in one call)"""

@@ -53,3 +53,31 @@ def test_oracle_parses_every_generated_macroblock(oracle, case):
     if mbw * mbh >= 99:
         assert seen_types == {0, 1, 2, 3, 4, 5, 6, 7}, seen_types   # every mb type class
         assert wraps > 0                                             # QP wrapped across 0 / 51
+
+
+@pytest.mark.parametrize('poc', [(1, 0), (1, 1), (2, 0)], ids=['poc1', 'poc1_always_zero', 'poc2'])
+def test_oracle_poc_types(oracle, poc):
+    """POC types 1 (with and without delta_pic_order_always_zero_flag) and 2: the slice header's POC
+    fields are parsed by the SPS's rules, every macroblock as generated"""
+    from streamgen import SyntaxGen
+    g = SyntaxGen(SO, 11, 9, 7, poc_type=poc[0], dpoaz=poc[1])
+    d = oracle.decoder()
+    units = []
+    for k in range(3):
+        units.append(((g.idr() if k == 0 else g.p()), g.log))
+    for k, (u, log) in enumerate(units):
+        rc, _, _, _ = d.decode(u)
+        assert rc == 1, f'unit {k}'
+        mi = np.zeros(11 * 9 * 8, np.int32)
+        oracle.L.h264o_dec_mbinfo(d.d, mi.ctypes.data)
+        assert [tuple(int(x) for x in r[:3]) for r in mi.reshape(-1, 8)] == log, f'unit {k}'
+
+
+def test_oracle_rejects_non_reference_picture(oracle):
+    """nal_ref_idc 0 (a non-reference P picture, which the wrapper's encoder never emits) is out of the
+    decoder's scope: rejected rather than misparsed (no dec_ref_pic_marking) or used as a reference"""
+    from streamgen import SyntaxGen
+    g = SyntaxGen(SO, 11, 9, 8)
+    d = oracle.decoder()
+    assert d.decode(g.idr())[0] == 1
+    assert d.decode(g.p(ref_idc=0))[0] != 1
