@@ -6,7 +6,10 @@ restatement of the reference path) on the bench's own geometry and bitrate befor
 with OpenH264 itself is unpinned. A failed check prints value null and exits 1.
 
 Default workload (the metric; at N > 1 also BASELINE.json configs[4]'s NAL gather): every rank owns
-S streams (default 8). One step = one frame of each of them: GPU encode (libh264mi batch encoder,
+S streams (default 32: the GPU's 1080p30 throughput comes from concurrent independent streams, SURVEY.md
+§7; at 32 streams a frame step of all of them takes ~13-15 ms, inside the 33 ms of a 30 fps frame
+interval, so every stream runs in real time -- the 8-stream line is kept in profiles/ beside it). One
+step = one frame of each of them: GPU encode (libh264mi batch encoder,
 IPPP, intra period 0, the wrapper's parameters, 1 Mbps) and GPU decode of exactly the NAL units
 produced, plus (N > 1) the gather of those NAL units to rank 0 over RCCL. Frames are encoded on one
 HIP stream and decoded in groups of G on another (entropy decoding of a group runs concurrently),
@@ -47,7 +50,8 @@ def parse():
     ap.add_argument('--steps', type=int, default=240)
     ap.add_argument('--warmup', type=int, default=16)
     ap.add_argument('--config', type=int, default=0, choices=[0, 2, 3, 4, 5], help='0 = the metric workload')
-    ap.add_argument('--streams', type=int, default=0, help='streams per GPU (default: 8; config 3: 1, config 5: 4)')
+    ap.add_argument('--streams', type=int, default=0,
+                    help='streams per GPU (default: 32 for the metric; config 3: 1, config 4: 8 decoders, config 5: 4)')
     ap.add_argument('--width', type=int, default=0)
     ap.add_argument('--height', type=int, default=0)
     ap.add_argument('--bitrate', type=int, default=1000000)
@@ -71,7 +75,7 @@ def parse():
     if a.config == 2:
         a.width, a.height = a.width or 1280, a.height or 720
     a.width, a.height = a.width or 1920, a.height or 1080
-    a.streams = a.streams or {3: 1, 5: 4}.get(a.config, 8)
+    a.streams = a.streams or {2: 8, 3: 1, 4: 8, 5: 4}.get(a.config, 32)
     a.group = a.group or (16 if a.config == 4 else 4)
     if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
         a.parse_cus = 24 if a.config in (0, 3, 5) else 0
@@ -491,7 +495,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
             3: 'IPPP encode+decode (intra period 0), one stream', 5: 'IPPP encode+decode (intra period 0)'}[a.config]
     cfg = {'workload': f'{W}x{H} {work}, {S} streams per GPU, {a.bitrate} bps, wrapper encoder params'
                        + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
-           'baseline_config': {0: 'metric (configs[2] x 8 streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
+           'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'parse_streams': a.parse_streams,
            'parallelism': f'streams x{world} (weak)'}
