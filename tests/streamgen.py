@@ -145,6 +145,7 @@ class SyntaxGen:
         self.crop = (crop_right, crop_bottom)
         self.cqp, self.init_qp = cqp, init_qp
         self.poc_type, self.dpoaz = poc_type, dpoaz  # POC type 0 / 1 (delta_pic_order_always_zero_flag) / 2
+        self.tc_choice = None  # TotalCoeff distribution of generated blocks (None: the default mix)
         self.frame_num = 0
         self.poc = 0
         self.idr_id = 0
@@ -203,7 +204,7 @@ class SyntaxGen:
         """coefficients in scan order (maxnum of them) for one block, bounded by QP"""
         rng = self.rng
         lim = max(1, 2048 // (25 << (qp // 6)))
-        tc = int(rng.choice([0, 1, 1, 2, 3, 4, 6, 8, maxnum // 2, maxnum]))
+        tc = int(rng.choice(self.tc_choice or [0, 1, 1, 2, 3, 4, 6, 8, maxnum // 2, maxnum]))
         tc = min(tc, maxnum)
         c = np.zeros(maxnum, np.int16)
         if tc:
@@ -310,7 +311,7 @@ class SyntaxGen:
         self._residual(w, nn, mx, my, cur, 'i16', cbpl | (cbpc << 4), qp, True)
         return qp, cur, None
 
-    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24, ref_idc=2):
+    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24, ref_idc=2, cbp_fixed=None):
         rng = self.rng
         mbw, mbh = self.mbw, self.mbh
         w = FastBits()
@@ -383,6 +384,8 @@ class SyntaxGen:
                         for _ in range({0: 1, 1: 2, 2: 2, 3: 4}[s]):
                             w.se(int(rng.integers(-max_mvd, max_mvd + 1))); w.se(int(rng.integers(-max_mvd, max_mvd + 1)))
                 cbp = int(rng.integers(0, 48)) if rng.random() < 0.85 else 0
+                if cbp_fixed is not None:
+                    cbp = cbp_fixed
                 w.ue(self.L.h264o_cbp_code(cbp, 0))
                 if cbp:
                     qp = self._qp_delta(w, qp)
