@@ -66,6 +66,9 @@ def parse():
     ap.add_argument('--parse-cus', type=int, default=-1,
                     help='CUs reserved for entropy decoding (CU mask bits [0, n) for the parse streams, the rest for the '
                          'encoder / reconstruction streams); 0 = shared; default 24 when encoding and decoding, else 0')
+    ap.add_argument('--recon-cus', type=int, default=0,
+                    help='CUs reserved for the reconstruction stream (mask bits [parse_cus, parse_cus + n)); the encoder '
+                         'keeps the rest. 0 = reconstruction shares the encoder\'s CUs')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
@@ -367,7 +370,10 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # on `ds`, takes G frames per call, entropy-decoding all G x S slices concurrently before
     # reconstructing them in order. NB staging buffers keep NB groups in flight: encoding group g+1
     # overlaps the entropy decoding of g and the reconstruction of g-1.
-    if a.parse_cus > 0:  # wavefront streams off the CUs reserved for entropy decoding
+    if a.parse_cus > 0 and a.recon_cus > 0:  # three lanes: entropy decoding, reconstruction, encoder
+        hi = a.parse_cus + a.recon_cus
+        es, ds = h264mi.masked_stream(0, hi, True), h264mi.masked_stream(a.parse_cus, hi, False)
+    elif a.parse_cus > 0:  # wavefront streams off the CUs reserved for entropy decoding
         es, ds = h264mi.masked_stream(0, a.parse_cus, True), h264mi.masked_stream(0, a.parse_cus, True)
     else:
         es, ds = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
@@ -497,7 +503,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                        + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
-           'parse_cus': a.parse_cus, 'parse_streams': a.parse_streams,
+           'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
