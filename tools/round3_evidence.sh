@@ -20,6 +20,7 @@ fi
 if [ "$part" = B ]; then
   timeout -k 10 200 python3 tools/capi_latency.py 1920 1080 1000000 12 > $out/capi_1m.log 2>&1 && j $out/capi_1m.log > $out/capi_1m.json
   timeout -k 10 200 python3 tools/capi_latency.py 1920 1080 8000000 12 > $out/capi_8m.log 2>&1 && j $out/capi_8m.log > $out/capi_8m.json
+  timeout -k 10 300 python3 tools/parse_mix.py > $out/parse_mix.txt 2>&1
   timeout -k 10 200 python3 tools/parse_prof.py 1920 1080 8000000 1 10 > $out/parse_prof_8m.txt 2>&1
   timeout -k 10 200 python3 tools/parse_prof.py 1920 1080 1000000 1 10 > $out/parse_prof_1m.txt 2>&1
   timeout -k 10 300 python3 tools/enc_prof.py 1920 1080 1000000 8 6 > $out/enc_sections.txt 2>&1
