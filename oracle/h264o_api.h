@@ -46,6 +46,7 @@ void h264o_dec_destroy(H264ODec *d);
  * error concealment), 0: no picture, -1: error with nothing to conceal */
 int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out_i420, int *w, int *h);
 void h264o_dec_mbinfo(const H264ODec *d, int32_t *out);
+void h264o_dec_nnz(const H264ODec *d, uint8_t *out);  /* 24 TotalCoeff bytes per MB of the last picture */
 
 /* test-stream helpers (tests/streamgen.py): CAVLC bits of one residual block (0/1 per byte; returns
  * the bit count, -1 if cap is too small) and the coded_block_pattern codeNum of cbp (Table 9-4) */

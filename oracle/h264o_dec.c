@@ -462,6 +462,10 @@ int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out, i
     d->has_ref = 1;
     return 1;
 }
+/* per MB the 24 TotalCoeff bytes (luma raster 0..15, chroma AC 16..23) of the last picture -- test / analysis */
+void h264o_dec_nnz(const H264ODec *d, uint8_t *out) {
+    for (int i = 0; i < d->mbw * d->mbh; i++) memcpy(out + 24 * i, d->mbs[i].nnz, 24);
+}
 void h264o_dec_mbinfo(const H264ODec *d, int32_t *out) {
     for (int i = 0; i < d->mbw * d->mbh; i++) {
         const MBInfo *m = &d->mbs[i];
