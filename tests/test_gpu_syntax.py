@@ -173,3 +173,37 @@ def test_config4_ring_fanout_1080p(gpu_lib, oracle):
         d.close()
     ring.close()
     enc.close()
+
+
+# macroblock contents that steer the asm P-slice run (cavlc_blk.inc p_mb_run) down each of its paths:
+# mix, fixed coded_block_pattern, TotalCoeff choices of the generated blocks
+ASM_KINDS = [
+    ('skip', {'skip': 1}, None, None),
+    ('p16_cbp0', {'p16': 1}, 0, None),
+    ('p16_chroma_dc', {'p16': 1}, 0x10, [0, 1, 2, 3, 4]),
+    ('p16_chroma_quiet', {'p16': 1}, 0x20, [0, 0, 0, 1]),      # quiet planes: empty blocks, tc 1 (short / long total_zeros)
+    ('p16_chroma_mixed', {'p16': 1}, 0x20, [0, 1, 2]),         # quiet planes that bail out, generic planes
+    ('p16_luma_dense', {'p16': 1}, 0x2f, [2, 4, 6, 16]),
+    ('p16_skip_i16', {'p16': 3, 'skip': 2, 'i16': 1}, None, None),  # runs, I_16x16 in P slices (DC + AC blocks)
+    ('p16_other_types', {'p16': 3, 'p16x8': 1, 'p8x8': 1, 'i4': 1, 'pcm': 0.3}, None, None),  # exits to the C++ loop
+]
+
+
+@pytest.mark.parametrize('kind', ASM_KINDS, ids=[k[0] for k in ASM_KINDS])
+def test_asm_p_run_paths_vs_oracle(gpu_lib, oracle, kind):
+    """P slices of one macroblock content each (CIF, IDR + 3 P pictures): every picture == the oracle
+    decoder's, through the C-ABI"""
+    from streamgen import SyntaxGen
+    name, mix, cbp, tcs = kind
+    g = SyntaxGen(SO, 22, 18, 31 + len(name))
+    g.tc_choice = tcs
+    units = [g.idr()] + [g.p(mix, cbp_fixed=cbp) for _ in range(3)]
+    od = oracle.decoder()
+    L = gpu_lib
+    assert L.init_decoder(15) == 0
+    for k, u in enumerate(units):
+        rc, pic, _, _ = od.decode(u)
+        assert rc == 1
+        gw, gh, got = gpu_decode(L, 15, u, 352, 288)
+        assert (gw, gh) == (352, 288) and np.array_equal(got, pic), f'{name} unit {k}'
+    L.deinit_decoder(15)
