@@ -65,7 +65,8 @@ def parse():
     ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
     ap.add_argument('--parse-cus', type=int, default=-1,
                     help='CUs reserved for entropy decoding (CU mask bits [0, n) for the parse streams, the rest for the '
-                         'encoder / reconstruction streams); 0 = shared; default 24 when encoding and decoding, else 0')
+                         'encoder / reconstruction streams); 0 = shared; default when encoding and decoding: 32 for >= 128 '
+                         'slices per call, else 24; 0 for decode-only')
     ap.add_argument('--recon-cus', type=int, default=0,
                     help='CUs reserved for the reconstruction stream (mask bits [parse_cus, parse_cus + n)); the encoder '
                          'keeps the rest. 0 = reconstruction shares the encoder\'s CUs')
@@ -81,7 +82,9 @@ def parse():
     a.streams = a.streams or {2: 8, 3: 1, 4: 8, 5: 4}.get(a.config, 32)
     a.group = a.group or (16 if a.config == 4 else 4)
     if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
-        a.parse_cus = 24 if a.config in (0, 3, 5) else 0
+        # a slice wave takes a quarter of a CU's LDS (four per CU): 32 CUs hold the 128 slices of a
+        # 32-stream, 4-frame call at once (24 CUs: two rounds); 40 measured slower (profiles/round3/pcus2)
+        a.parse_cus = (32 if a.streams * a.group >= 128 else 24) if a.config in (0, 3, 5) else 0
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.

@@ -47,16 +47,20 @@ def test_encoder_matches_oracle_and_fixture(gpu_lib, oracle, case):
 
 
 def test_encoder_1080p_ippp_fixture_free(gpu_lib, oracle):
-    """config 3 slice: 1920x1080 IPPP at 1 Mbps, 3 frames, GPU bytes == oracle bytes"""
+    """config 3 slice: 1920x1080 IPPP, 3 frames, GPU bytes == oracle bytes. At 8 Mbps: with the wrapper's
+    frame skipping on, 1 Mbps skips the two P frames after the IDR (profiles/round3/final/capi_1m.json),
+    so this bitrate is the one whose P frames are actually coded (asserted non-empty)."""
     from h264mi.synth import SyntheticStream
     w, h = 1920, 1080
     L = gpu_lib
-    assert L.init_encoder(w, h, 1000000) == 0
-    oe = oracle.encoder(w, h, 1000000)
+    assert L.init_encoder(w, h, 8000000) == 0
+    oe = oracle.encoder(w, h, 8000000)
     g = SyntheticStream(0, w, h)
     for t in range(3):
         f = np.ascontiguousarray(g.frame(t))
-        assert gpu_encode(L, f, w, h) == oe.encode(f), t
+        got = gpu_encode(L, f, w, h)
+        assert len(got) > 0, t
+        assert got == oe.encode(f), t
 
 
 def test_encoder_rejects_bad_geometry(gpu_lib):
