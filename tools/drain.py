@@ -4,7 +4,7 @@ K-th-last enc_mb_kernel).  usage: drain.py <run_kernel_trace.csv> [K]"""
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0].replace('h264mi::', '')) for r in rows)
+ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0].split('<')[0].replace('void ', '').replace('h264mi::', '')) for r in rows)
 enc = [e for e in ev if e[2] == 'enc_mb_kernel']
 t0 = enc[-K][0]
 ms = lambda t: (t - t0) / 1e6
