@@ -106,9 +106,32 @@ def relaunch(a):
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
+# the reference's only published numbers (a screenshot: wasm OpenH264 at 854x480, 1 Mbps)
+# scaled by macroblock count to 1080p give, per core of that machine, ~79 encodes/s and ~41.7
+# encode+decode frames/s. An estimate of OpenH264's CPU speed, not a measurement (OpenH264 itself is
+# never run here).
+OPENH264_1080P_PER_CORE = {'encdec': 41.7, 'encode': 79.0}
+
+
+def openh264_estimate(a, cores):
+    """the screenshot-implied OpenH264 rate on the box's cores for the metric's 1080p IPPP encode+decode
+    configs (None for the I-only and decode-only configs, which the screenshot does not price)"""
+    if a.config not in (0, 3, 5) or (a.width, a.height) != (1920, 1080) or not cores:
+        return None
+    return {'value': OPENH264_1080P_PER_CORE['encdec'] * cores, 'encode_only': OPENH264_1080P_PER_CORE['encode'] * cores,
+            'unit': 'frames/s', 'cores': cores, 'kind': 'estimate',
+            'basis': 'BASELINE.md §1: screenshot-implied per-core 1080p rates of the reference\'s wasm OpenH264 '
+                     '(41.7 encode+decode, 79 encode-only frames/s per core) x the box\'s cores, assuming linear '
+                     'scaling over independent streams; an estimate, not a measurement'}
+
+
 def cpu_baseline(a, mode):
+    """the CPU leg (a child process, before this process touches the GPU): the timed baseline, plus the
+    oracle's hashes of the first parity_frames frames of every stream the timed pipeline encodes"""
     cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
            '--bitrate', str(a.bitrate), '--frames', str(a.cpu_frames), '--mode', mode, '--hash', str(a.parity_frames)]
+    if mode != 'dec':
+        cmd += ['--hash-streams', str(a.streams)]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])
@@ -199,15 +222,17 @@ def measure_traffic(a):
                  f'loads, so 2 x FETCH_SIZE is an upper bound on its reads and the raw counters ({raw / 1e6:.1f} MB) a lower bound')
 
 
-def oracle_hashes(a, mode, sid):
-    """the oracle's sha256 of synthetic stream sid's first frames (N > 1 ranks; child process, no GPU)"""
+def oracle_hashes(a, mode, first):
+    """the oracle's sha256 of the first frames of this rank's streams first..first+S-1 (N > 1 ranks;
+    child process, no GPU): {str(stream id): [{'nal', 'pic'}, ...]}"""
     cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
-           '--bitrate', str(a.bitrate), '--mode', mode, '--hash', str(a.parity_frames), '--hash-stream', str(sid), '--hash-only']
+           '--bitrate', str(a.bitrate), '--mode', mode, '--hash', str(a.parity_frames), '--hash-first', str(first),
+           '--hash-streams', str(a.streams), '--hash-only']
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
-        return json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])['parity_hashes']
+        return json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])['parity_hashes_streams']
     except Exception:
-        return []  # reported as a failed parity check (no hashes)
+        return {}  # reported as a failed parity check (no hashes)
 
 
 def gpu_parity(a, oracle_hashes, i_only=False, sid=0):
@@ -240,6 +265,25 @@ def gpu_parity(a, oracle_hashes, i_only=False, sid=0):
     return ok, f'stream {sid} frames 0..{len(oracle_hashes) - 1}: ' + ('pass' if ok else 'FAIL')
 
 
+def all_stream_parity(captured, shashes, sids, a, decoded):
+    """frames 0..K-1 of every stream of the timed pipeline (captured during its warmup) vs the oracle's
+    sha256 of the same synthetic streams: NAL bytes, and decoded pictures when the pipeline decodes"""
+    K = a.parity_frames
+    if not captured:
+        return False, f'not checked (warmup {a.warmup} < {K} frames, or no capture)'
+    bad = []
+    for s, sid in enumerate(sids):
+        want = shashes.get(str(sid)) or []
+        got = captured.get(s) or []
+        ok = len(want) == K and len(got) == K and all(
+            g['nal'] == w['nal'] and (not decoded or g['pic'] == w['pic']) for g, w in zip(got, want))
+        if not ok:
+            bad.append(sid)
+    what = 'NAL bytes' + (' and decoded pictures' if decoded else '')
+    msg = f'{len(sids)} streams x {K} frames of the timed pipeline ({what}) vs the oracle: '
+    return not bad, msg + ('pass' if not bad else f'FAIL (streams {bad[:8]})')
+
+
 def timed(run_steps, K, W, dist, sync):
     run_steps(W)
     sync()
@@ -269,12 +313,13 @@ def main():
     mode = {2: 'enc_i', 4: 'dec'}.get(a.config, 'encdec')
     # CPU baseline + oracle parity hashes first, in child processes, before this process touches the GPU.
     # At N > 1 every rank takes the oracle's hashes of its own first stream (no timing).
-    cpu, hashes = None, None
+    cpu, hashes, shashes = None, None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, mode)
         hashes = cpu.get('parity_hashes')
+        shashes = cpu.get('parity_hashes_streams')
     elif world > 1 and not a.no_cpu_baseline:
-        hashes = oracle_hashes(a, mode, rank * a.streams)
+        shashes = oracle_hashes(a, mode, rank * a.streams)
     a.traffic_kernel = 'dec_recon_kernel' if a.config == 4 else 'enc_mb_kernel'
     a.traffic_measured = (None, 'not measured (--no-traffic or N > 1)')
     if rank == 0 and world == 1 and not a.no_traffic:
@@ -298,15 +343,21 @@ def main():
     if a.config == 4:
         res = bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync)
     else:
-        res = bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank)
-    # the oracle parity check runs after the timed region: its own encoder and decoder (and their HIP
-    # streams) would otherwise exist before the timed pipeline's streams are created. At N > 1 each rank
-    # checks its own first stream.
+        # parity: the timed pipeline's own encoder and decoder, every stream, frames 0..K-1 (captured in
+        # the warmup, which starts at frame 0) against the oracle's hashes of the same streams
+        cap = a.parity_frames if shashes is not None and a.warmup >= a.parity_frames else 0
+        res = bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank, cap)
     parity_ok, parity_msg = True, 'skipped (--no-cpu-baseline)'
-    if hashes is not None:
-        parity_ok, parity_msg = gpu_parity(a, hashes, i_only=a.config == 2, sid=rank * a.streams)
+    if a.config == 4 and hashes is not None:
+        # decode-only: the bench's stream 0 (its decoders all decode that stream) from a fresh encoder +
+        # decoder after the timed region
+        parity_ok, parity_msg = gpu_parity(a, hashes, sid=0)
+    elif shashes is not None:
+        parity_ok, parity_msg = all_stream_parity(res.pop('captured', None), shashes, stream_ids(rank, a.streams), a,
+                                                  decoded=a.config != 2)
         if world > 1:
-            parity_msg = f'rank {rank} (stream {rank * a.streams}) ' + parity_msg
+            parity_msg = f'rank {rank}: ' + parity_msg
+    res.pop('captured', None)
     parity_ok = parity_ok and res.pop('selfcheck_ok')
     elapsed = res.pop('elapsed')
     if dist:
@@ -316,19 +367,28 @@ def main():
         ok = torch.tensor([1 if parity_ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity_ok = bool(ok.item())
-        if hashes is not None:
-            parity_msg = f'all {world} ranks, each its first stream vs the oracle: ' + ('pass' if parity_ok else 'FAIL')
+        if shashes is not None:
+            parity_msg = (f'all {world} ranks x {a.streams} streams x {a.parity_frames} frames of the timed pipeline vs the '
+                          'oracle: ' + ('pass' if parity_ok else 'FAIL'))
     frames = res.pop('frames_per_rank') * world
     value = frames / elapsed
     if rank == 0:
+        vs = None
         if cpu is not None:
             cpu = {k: cpu.get(k) for k in ('value', 'unit', 'cores', 'kind', 'sample', 'value_1core', 'build', 'encode_only')
                    if k in cpu}
+            est = openh264_estimate(a, cpu.get('cores'))
+            if est is not None:
+                cpu['openh264_estimate'] = est
+                vs = value / est['value'] if parity_ok else None
+                cpu['ratios'] = {'value_over_openh264_estimate': vs,
+                                 'value_over_openh264_encode_estimate': value / est['encode_only'] if parity_ok else None,
+                                 'value_over_restatement': value / cpu['value'] if parity_ok and cpu.get('value') else None}
         out = {
             'metric': METRIC + ' (parity vs oracle; OpenH264 parity unpinned)',
             'value': value if parity_ok else None, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+            'vs_baseline': vs, 'dtype': 'u8', 'data': 'synthetic',
             'config': res.pop('config'),
             'roofline': res.pop('roofline'),
             'cpu_baseline': cpu,
@@ -357,8 +417,9 @@ def roofline(kernel, alg_bytes, ms_total, launches, a, note=None):
     return r
 
 
-def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank):
-    """configs 0 (metric), 2 (I-only encode), 3 (one stream), 5 (4 streams): encode (+ decode)"""
+def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, dev, sync, dist, world, rank, capture=0):
+    """configs 0 (metric), 2 (I-only encode), 3 (one stream), 5 (4 streams): encode (+ decode). capture = K:
+    the warmup keeps every stream's NAL units and decoded pictures of frames 0..K-1 (parity check)"""
     W, H, S, G = a.width, a.height, a.streams, a.group
     F = W * H * 3 // 2
     i_only = a.config == 2
@@ -400,6 +461,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # only (a stream of their own), never after its decode: NalGather's host reads are one group late
     gs = torch.cuda.Stream(device=dev) if gather is not None else None
     state = {'t': 0, 'g': 0}
+    cap_nal = []  # (stage copy, sizes copy) of frames 0..capture-1
+    cap_pic = torch.empty((capture, S, W * H * 3 // 2), dtype=torch.uint8, device=dev) if capture and decode else None
 
     def run_group(n):
         b = state['g'] % NB
@@ -413,6 +476,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                     enc.force_idr(-1)
                 enc.encode(clip[(t0 + j) % a.clip])
                 enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
+                if t0 + j < capture:
+                    cap_nal.append((stage[b][j].clone(), stage_sz[b][j].clone()))
             ev_enc[b].record(es)
         state['t'] = t0 + n
         with torch.cuda.stream(ds):
@@ -421,7 +486,10 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                 base = stage[b].data_ptr()
                 ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
                 szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
-                dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b])
+                outp = None
+                if t0 < capture:  # every frame's picture of the first frames (parity capture, warmup only)
+                    outp = [cap_pic[t0 + j, s].data_ptr() if t0 + j < capture else 0 for j in range(n) for s in range(S)]
+                dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b], out_ptrs=outp)
             ev_dec[b].record(ds)
         if gather is not None:
             with torch.cuda.stream(gs):
@@ -447,6 +515,21 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # warmup, then the self-check: decoder output == encoder reconstruction, every stream
     run_steps(a.warmup)
     sync()
+    captured = None
+    if capture:
+        captured = {s: [] for s in range(S)}
+        pics = cap_pic.cpu().numpy() if cap_pic is not None else None
+        for t, (nb, sz) in enumerate(cap_nal):
+            szh = sz.cpu().tolist()
+            host = nb.cpu().numpy()
+            for s in range(S):
+                e = {'nal': hashlib.sha256(host[s * slot:s * slot + szh[s]].tobytes()).hexdigest()}
+                if pics is not None:
+                    e['pic'] = hashlib.sha256(pics[t, s].tobytes()).hexdigest()
+                captured[s].append(e)
+        del pics
+        cap_nal.clear()
+        cap_pic = None
     selfcheck_ok = True
     if decode:
         rc, got = dec.status()
@@ -510,7 +593,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
-    return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg,
+    return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg, 'captured': captured,
             'roofline': roofline('enc_mb_kernel', alg, ems, en, a), 'kernels': kern,
             'nal_gather': gather_check,
             'selfcheck_ok': selfcheck_ok,

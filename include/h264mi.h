@@ -87,7 +87,8 @@ int h264mi_enc_encode(h264mi_encoder *e, const void *d_frames);     /* async; ns
 int h264mi_enc_set_frame_skip(h264mi_encoder *e, int enable);
 int h264mi_enc_frames_skipped(h264mi_encoder *e, int stream);
 /* test hook: the next coded frame of stream fails as if its kernels had reported error code (> 0): it
-   publishes 0 NAL bytes and the frame after it is an IDR */
+   publishes 0 NAL bytes and the frame after it is an IDR. Code 3 fails it through enc_pack_kernel's
+   RBSP-overflow branch itself (the early exit before the slice is assembled) */
 int h264mi_enc_inject_error(h264mi_encoder *e, int stream, int code);
 int h264mi_enc_sync(h264mi_encoder *e);
 int h264mi_enc_nal_bytes(h264mi_encoder *e, int *out_bytes);        /* sync; -2 if a kernel reported an error */

@@ -27,8 +27,11 @@ namespace h264mi {
 constexpr uint8_t ZZ[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};       // Table 8-13
 constexpr uint8_t BLK2RAS[16] = {0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15};  // 6.4.3
 constexpr uint8_t POSCLS[16] = {0, 2, 0, 2, 2, 1, 2, 1, 0, 2, 0, 2, 2, 1, 2, 1};
-__constant__ const int32_t c_MF[6][3] = {{13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554},
-                                        {9362, 3647, 5825},  {8192, 3355, 5243},  {7282, 2893, 4559}};
+// OpenH264's quantiser tables (g_kiQuantMF / g_kiQuantInterFF as the reference's h264.wasm holds them,
+// tests/golden/openh264_tables.json), one entry per coefficient class
+// {even/even, odd/odd, mixed} = positions {0, 5, 1} of the 8-wide rows. FF: inter rows qp, intra qp + 6.
+__constant__ const int32_t c_QMF[52][3] = {{26214, 10486, 16132}, {23832, 9320, 14980}, {20164, 8388, 13108}, {18724, 7294, 11650}, {16384, 6710, 10486}, {14564, 5786, 9118}, {13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554}, {9362, 3647, 5825}, {8192, 3355, 5243}, {7282, 2893, 4559}, {6554, 2622, 4033}, {5958, 2330, 3745}, {5041, 2097, 3277}, {4681, 1824, 2913}, {4096, 1678, 2622}, {3641, 1447, 2280}, {3277, 1311, 2017}, {2979, 1165, 1873}, {2521, 1049, 1639}, {2341, 912, 1456}, {2048, 839, 1311}, {1821, 723, 1140}, {1638, 655, 1008}, {1490, 583, 936}, {1260, 524, 819}, {1170, 456, 728}, {1024, 419, 655}, {910, 362, 570}, {819, 328, 504}, {745, 291, 468}, {630, 262, 410}, {585, 228, 364}, {512, 210, 328}, {455, 181, 285}, {410, 164, 252}, {372, 146, 234}, {315, 131, 205}, {293, 114, 182}, {256, 105, 164}, {228, 90, 142}, {205, 82, 126}, {186, 73, 117}, {158, 66, 102}, {146, 57, 91}, {128, 52, 82}, {114, 45, 71}, {102, 41, 63}, {93, 36, 59}, {79, 33, 51}, {73, 28, 46}};
+__constant__ const int32_t c_QFF[58][3] = {{0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 2, 1}, {1, 2, 1}, {1, 2, 1}, {1, 2, 1}, {1, 3, 2}, {1, 3, 2}, {1, 3, 2}, {1, 4, 2}, {2, 4, 3}, {2, 5, 3}, {2, 5, 3}, {2, 6, 4}, {3, 7, 4}, {3, 8, 5}, {3, 8, 5}, {4, 9, 6}, {4, 10, 7}, {5, 12, 8}, {5, 13, 8}, {6, 15, 10}, {7, 17, 11}, {7, 19, 12}, {9, 21, 13}, {9, 24, 15}, {11, 26, 17}, {12, 30, 19}, {13, 33, 22}, {15, 38, 23}, {17, 42, 27}, {19, 48, 30}, {21, 52, 33}, {24, 60, 38}, {27, 67, 43}, {29, 75, 47}, {35, 83, 53}, {37, 96, 60}, {43, 104, 67}, {48, 121, 77}, {53, 133, 87}, {59, 150, 93}, {69, 167, 107}, {75, 192, 120}, {85, 208, 133}, {96, 242, 153}, {107, 267, 173}, {117, 300, 187}, {139, 333, 213}, {149, 383, 240}, {171, 417, 267}, {192, 483, 307}, {213, 533, 347}, {235, 600, 373}, {277, 667, 427}, {299, 767, 480}};
 __constant__ const int32_t c_V[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
 __constant__ const uint8_t c_CHROMA_QP[52] = {
     0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
@@ -49,22 +52,31 @@ DEV int se_len(int v) { return ue_len(v > 0 ? (uint32_t)(2 * v - 1) : (uint32_t)
 
 // Quantisation constants for one QP (uniform per frame)
 struct QuantQP {
-    int mf0, mf1, mf2, v0, v1, v2, q6, qbits, fintra, finter;
+    int mf0, mf1, mf2, fi0, fi1, fi2, fp0, fp1, fp2, v0, v1, v2, q6;
 };
 DEV QuantQP make_qqp(int qp) {
     QuantQP q;
     int r = qp % 6;
-    q.mf0 = c_MF[r][0]; q.mf1 = c_MF[r][1]; q.mf2 = c_MF[r][2];
+    q.mf0 = c_QMF[qp][0]; q.mf1 = c_QMF[qp][1]; q.mf2 = c_QMF[qp][2];
+    q.fi0 = c_QFF[qp + 6][0]; q.fi1 = c_QFF[qp + 6][1]; q.fi2 = c_QFF[qp + 6][2];
+    q.fp0 = c_QFF[qp][0]; q.fp1 = c_QFF[qp][1]; q.fp2 = c_QFF[qp][2];
     q.v0 = c_V[r][0]; q.v1 = c_V[r][1]; q.v2 = c_V[r][2];
-    q.q6 = qp / 6; q.qbits = 15 + q.q6;
-    q.fintra = (1 << q.qbits) / 3; q.finter = (1 << q.qbits) / 6;
+    q.q6 = qp / 6;
     return q;
 }
+// per-lane class selects of single fields (a select of the struct or of an array would go through scratch)
+DEV int qmf(const QuantQP &q, int cls) { return cls == 0 ? q.mf0 : (cls == 1 ? q.mf1 : q.mf2); }
+DEV int qff(const QuantQP &q, int cls, int intra) {
+    const int f0 = intra ? q.fi0 : q.fp0, f1 = intra ? q.fi1 : q.fp1, f2 = intra ? q.fi2 : q.fp2;  // uniform
+    return cls == 0 ? f0 : (cls == 1 ? f1 : f2);
+}
 template <int POS> DEV int mf_of(const QuantQP &q) { return POSCLS[POS] == 0 ? q.mf0 : (POSCLS[POS] == 1 ? q.mf1 : q.mf2); }
+template <int POS> DEV int ff_of(const QuantQP &q, int intra) { return qff(q, POSCLS[POS], intra); }
 template <int POS> DEV int v_of(const QuantQP &q) { return POSCLS[POS] == 0 ? q.v0 : (POSCLS[POS] == 1 ? q.v1 : q.v2); }
-// 32-bit is exact here: |c| <= 9180 (4x4 transform of 8-bit residuals), mf <= 13107, f < 2^23
-DEV int quant1(int c, int mf, int qbits, int f) {
-    int l = (int)(((uint32_t)iabs(c) * (uint32_t)mf + (uint32_t)f) >> qbits);
+// OpenH264's quantiser (WelsQuant4x4_c): level = sign(c) * (((|c| + ff) * mf) >> 16). 32-bit exact:
+// |c| <= 9180 (4x4 transform of 8-bit residuals), ff <= 767, mf <= 26214
+DEV int quant1(int c, int mf, int ff) {
+    int l = (int)((((uint32_t)iabs(c) + (uint32_t)ff) * (uint32_t)mf) >> 16);
     return c < 0 ? -l : l;
 }
 
@@ -115,12 +127,12 @@ DEV int satd4(const int d[16]) {
     return (s + 1) >> 1;
 }
 // quantise a raster coefficient block into scan-ordered levels (positions >= first); returns TotalCoeff
-DEV int quant_block(const int c[16], const QuantQP &q, int f, int first, int16_t lv[16]) {
+DEV int quant_block(const int c[16], const QuantQP &q, int intra, int first, int16_t lv[16]) {
     int n = 0;
-#define QK(K)                                                                          \
-    {                                                                                  \
-        int l = (K) >= first ? quant1(c[ZZ[K]], mf_of<ZZ[K]>(q), q.qbits, f) : 0;      \
-        lv[K] = (int16_t)l; n += l != 0;                                               \
+#define QK(K)                                                                                   \
+    {                                                                                           \
+        int l = (K) >= first ? quant1(c[ZZ[K]], mf_of<ZZ[K]>(q), ff_of<ZZ[K]>(q, intra)) : 0;   \
+        lv[K] = (int16_t)l; n += l != 0;                                                        \
     }
     QK(0) QK(1) QK(2) QK(3) QK(4) QK(5) QK(6) QK(7) QK(8) QK(9) QK(10) QK(11) QK(12) QK(13) QK(14) QK(15)
 #undef QK
@@ -132,9 +144,11 @@ DEV void dequant_block(const int16_t lv[16], const QuantQP &q, int c[16]) {
     DK(0) DK(1) DK(2) DK(3) DK(4) DK(5) DK(6) DK(7) DK(8) DK(9) DK(10) DK(11) DK(12) DK(13) DK(14) DK(15)
 #undef DK
 }
-// DC terms: |v| <= 32640 (luma, after >> 1) or 16320 (chroma): |v| * mf0 + 2f < 2^32
-DEV int quant_dc(int v, int mf0, int qbits, int f) {
-    int l = (int)(((uint32_t)iabs(v) * (uint32_t)mf0 + 2u * (uint32_t)f) >> (qbits + 1));
+// DC levels (I16x16 luma DC after the Hadamard, chroma 2x2 DC): OpenH264 quantises them with
+// (int16)(FF[0] << 1) and MF[0] >> 1 (WelsQuant4x4Dc / WelsHadamardQuant2x2). |v| <= 32640 (luma) or
+// 16320 (chroma): (|v| + 2 ff0) * (mf0 >> 1) < 2^31
+DEV int quant_dc(int v, int mf0, int ff0) {
+    int l = (int)((((uint32_t)iabs(v) + 2u * (uint32_t)ff0) * ((uint32_t)mf0 >> 1)) >> 16);
     return v < 0 ? -l : l;
 }
 // 8.5.10 luma DC scaling of one inverse-Hadamard output

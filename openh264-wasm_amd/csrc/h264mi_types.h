@@ -66,6 +66,10 @@ struct EncState {
     int32_t skip_en;       // frame skipping enabled (the wrapper's default)
     int32_t skipped;       // frames skipped so far
     int32_t inject_err;    // test hook (h264mi_enc_inject_error): the next coded frame fails with this code
+                           // (3: through the RBSP-overflow branch of enc_pack_kernel)
+    // rate control state beside qp (oracle rc_frame_qp): the first IDR's table QP and
+    // the IDR QP range (RcCalculateIdrQp), IDRs / P frames coded, the coded frame's QP window
+    int32_t init_qp, rmin, rmax, idr_num, pframes, cur_qmin, cur_qmax;
     int32_t sps_bytes, pps_bytes;
     uint8_t sps[64], pps[32];
 };
@@ -93,7 +97,7 @@ struct EncDesc {
     int32_t ps, psc;        // row strides of pl / plc
     int32_t pad3[2];
     uint64_t *egran;        // MB -> deblocking hand-off, 128 granules per MB (deblock.inc DbkSrcGranules)
-    int32_t *rowqp;         // MB-row (GOM) QP plan of the frame being coded (written by the previous pack)
+    int32_t *rowqp;         // MB-row (GOM) QP offsets of the frame being coded (written by the previous pack)
     int32_t *rowbits;       // macroblock_layer() bits per MB row of the last coded frame
     uint64_t *rowq;         // per MB row: {epoch, QPY entering the row} granules (row r publishes r + 1)
 };

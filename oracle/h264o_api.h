@@ -35,6 +35,9 @@ int h264o_enc_frames_skipped(const H264OEnc *e);
 void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]);
 int h264o_rc_row_delta(int64_t row_bits, int64_t mean);
 int h264o_rc_init_qp(int w, int h, int bitrate);
+int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax);  /* first IDR QP, IDR QP range */
+void h264o_rc_constants(int32_t out[8]);  /* fps, QP min/max, frame window lower/upper, IDR window, IDR ratio, skip ratio */
+int h264o_table(const char *name, double *out);  /* the oracle's copy of an OpenH264 table (entry count, -1 unknown) */
 int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr);
 size_t h264o_write_sps(int w, int h, uint8_t *out);
 size_t h264o_write_pps(uint8_t *out);

@@ -119,14 +119,21 @@ void idct4_add(const int c[16], uint8_t *dst, int stride, const uint8_t *pred, i
         dst[3 * stride + j] = (uint8_t)clip1(pred[3 * pstride + j] + ((r3 + 32) >> 6));
     }
 }
-/* Quantiser: level = sign(c) * ((|c| * MF + f) >> (15 + qp/6)),
- * f = 2^qbits / 3 (intra) or / 6 (inter). */
+/* Quantiser: OpenH264's table quantiser (WelsQuant4x4_c; tables from h264.wasm):
+ * level = sign(c) * (((|c| + FF) * MF) >> 16), MF = OH_QUANT_MF[qp][pos & 7], FF = OH_QUANT_FF[qp +
+ * 6 * intra][pos & 7] (intra rounding rows sit six rows down, wasm funcs 345 / 536). pos: raster. */
 int quant4(int c, int qp, int pos, int intra) {
-    int qbits = 15 + qp / 6;
-    int f = (1 << qbits) / (intra ? 3 : 6);
     int a = iabs(c);
-    int l = (int)(((int64_t)a * QUANT_MF[qp % 6][POS_CLASS[pos]] + f) >> qbits);
+    int l = ((a + OH_QUANT_FF[qp + (intra ? 6 : 0)][pos & 7]) * OH_QUANT_MF[qp][pos & 7]) >> 16;
     return c < 0 ? -l : l;
+}
+/* DC levels (I16x16 luma DC after the Hadamard, chroma 2x2 DC): WelsQuant4x4Dc / WelsHadamardQuant2x2
+ * called with (int16)(FF[0] << 1) and MF[0] >> 1 (wasm funcs 265, 345, 534). */
+int quant_dc4(int v, int qp, int intra) {
+    int a = iabs(v);
+    int ff = (int16_t)(OH_QUANT_FF[qp + (intra ? 6 : 0)][0] << 1), mf = OH_QUANT_MF[qp][0] >> 1;
+    int l = ((a + ff) * mf) >> 16;
+    return v < 0 ? -l : l;
 }
 /* SATD: (sum |H d H| + 1) >> 1 over a 4x4 difference block. */
 int satd4(const int d[16]) {

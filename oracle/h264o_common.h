@@ -70,6 +70,7 @@ int br_more_rbsp(BR *r);
 void fdct4(const int d[16], int c[16]);                 /* forward core transform */
 void idct4_add(const int c[16], uint8_t *dst, int stride, const uint8_t *pred, int pstride); /* 8.5.12 */
 int quant4(int c, int qp, int pos, int intra);
+int quant_dc4(int v, int qp, int intra);
 int satd4(const int d[16]);
 void dequant_block(const int16_t lvl_scan[16], int qp, int first, int out_raster[16]);
 void luma_dc_dequant(const int16_t lvl_scan[16], int qp, int dc_raster[16]);   /* 8.5.10 */

@@ -17,9 +17,15 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define RC_FPS 30
-#define QP_MIN 12
-#define QP_MAX 51
+/* Rate-control constants OpenH264 applies at the wrapper's parameters, as its h264.wasm holds them
+ * (tests/golden/openh264_tables.json "code_constants"): */
+#define RC_FPS 60           /* GetDefaultParams fMaxFrameRate (wasm func 1023); the wrapper never sets it */
+#define QP_MIN 12           /* iMinQp / iMaxQp for camera content when the caller leaves iMinQp 0 (func 597) */
+#define QP_MAX 42
+#define FRAME_DQP_LOWER 3   /* iFrameDeltaQpLower / iFrameDeltaQpUpper at iRcVaryRatio 0 (func 592) */
+#define FRAME_DQP_UPPER 5
+#define IDR_QP_WINDOW 3     /* RcCalculateIdrQp: the IDR's frame QP window (func 1226) */
+#define LEVEL_FPS 30        /* level_idc choice (this project's rule; not pinned) */
 #define LOG2_MAX_FRAME_NUM 16
 #define LOG2_MAX_POC_LSB 16
 #ifndef CROSS_THR
@@ -33,11 +39,14 @@ struct H264OEnc {
     MBInfo *mbs;
     int first, force_idr;
     int frame_num, idr_pic_id, poc;
-    int qp;
+    int qp;           /* the next frame's QP before its bounds (the bits-ratio step below) */
     int last_qp, last_idr;
+    int init_qp, rmin, rmax;  /* RcCalculateIdrQp: first IDR QP and the IDR QP range */
+    int idr_num, pframes;     /* IDRs / P frames coded (OpenH264 iIdrNum, iPFrameNum) */
+    int qmin, qmax;           /* the coded frame's QP window (iMinFrameQp, iMaxFrameQp): clamps the row QPs */
     int64_t last_bits;
     /* GOM (MB-row) rate control and frame skipping */
-    int *rowqp;       /* QP plan of the next frame, one per MB row */
+    int *rowqp;       /* QP offset plan of the next frame, one per MB row (added to the frame QP) */
     int64_t *rowbits; /* macroblock_layer() bits per MB row of the last coded frame */
     int64_t vbuf;     /* virtual buffer fullness (bits) */
     int skip_en, skipped;
@@ -45,17 +54,30 @@ struct H264OEnc {
 };
 
 /* ---------------- rate control ---------------- */
-int h264o_rc_init_qp(int w, int h, int bitrate) {
-    int64_t bpf = bitrate / RC_FPS;
-    int64_t mbpp = bpf * 1000 / ((int64_t)w * h);
-    if (mbpp >= 600) return 20;
-    if (mbpp >= 400) return 24;
-    if (mbpp >= 200) return 28;
-    if (mbpp >= 100) return 32;
-    if (mbpp >= 50) return 36;
-    if (mbpp >= 25) return 40;
-    return 44;
+/* RcCalculateIdrQp restated from the reference's h264.wasm (func 1226, file offsets 766934-767578):
+ * bits per pixel = bitrate / (float)(fps * w * h); area class by w * h; the first column i of
+ * OH_RC_BPP[class] at or above it (the search starts at column 0: bFixRCOverShoot defaults to 1);
+ * IDR QP range = OH_RC_QP_RANGE[i] clipped to [QP_MIN, QP_MAX]; first IDR QP = OH_RC_INIT_QP[class][i]
+ * clipped to that range. Writes *rmin / *rmax, returns the first IDR QP. */
+int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax) {
+    float p = (float)RC_FPS * (float)w;
+    p = p * (float)h;
+    const double bpp = (double)bitrate / (double)p;
+    const int area = w * h;
+    const int cls = area < 28801 ? 0 : (area < 115201 ? 1 : (area < 460801 ? 2 : 3));
+    int i = 0;
+    while (i < 4 && !(OH_RC_BPP[cls][i] >= bpp)) i++;
+    const int mx = clip3(QP_MIN, QP_MAX, OH_RC_QP_RANGE[i][0]), mn = clip3(QP_MIN, QP_MAX, OH_RC_QP_RANGE[i][1]);
+    *rmin = mn; *rmax = mx;
+    return clip3(mn, mx, OH_RC_INIT_QP[cls][i]);
 }
+int h264o_rc_init_qp(int w, int h, int bitrate) {
+    int a, b;
+    return h264o_rc_idr_params(w, h, bitrate, &a, &b);
+}
+/* The next frame's QP before its bounds: this project's step on the bits of the frame just coded
+ * against the per-frame target T = bitrate / fps (x4 for an IDR: iIdrBitrateRatio 400). OpenH264
+ * derives it from its complexity model instead (RcCalculatePictureQp); not pinned. */
 int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr) {
     int64_t T = bitrate / RC_FPS;
     if (was_idr) T *= 4;
@@ -68,8 +90,31 @@ int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr) {
     else d = 0;
     return clip3(QP_MIN, QP_MAX, qp + d);
 }
-/* MB-row ("GOM") QP plan of the next frame around its frame QP: rows that cost more than the mean
- * in the last coded frame are quantised more coarsely, cheaper rows more finely. */
+/* The coded frame's QP and window (RcCalculateIdrQp / RcCalculatePictureQp, wasm func 1226):
+ * IDR: the first takes the table QP, later ones the step result, clipped to the IDR range; window
+ * QP -/+ IDR_QP_WINDOW inside the range. P: the first P frame takes the first IDR's QP, later ones
+ * the step result; window [last - FRAME_DQP_LOWER, last + FRAME_DQP_UPPER] inside [QP_MIN, QP_MAX],
+ * last = the previous coded frame's QP; the QP is clipped to the window. */
+static int rc_frame_qp(H264OEnc *e, int idr) {
+    int q;
+    if (idr) {
+        q = e->idr_num == 0 ? e->init_qp : clip3(e->rmin, e->rmax, e->qp);
+        e->qmin = clip3(e->rmin, e->rmax, q - IDR_QP_WINDOW);
+        e->qmax = clip3(e->rmin, e->rmax, q + IDR_QP_WINDOW);
+        e->idr_num++;
+    } else {
+        q = e->pframes == 0 ? e->init_qp : e->qp;
+        e->qmin = clip3(QP_MIN, QP_MAX, e->last_qp - FRAME_DQP_LOWER);
+        e->qmax = clip3(QP_MIN, QP_MAX, e->last_qp + FRAME_DQP_UPPER);
+        q = clip3(e->qmin, e->qmax, q);
+        e->pframes++;
+    }
+    return q;
+}
+/* MB-row ("GOM") QP offsets of the next frame: rows that cost more than the mean in the last coded
+ * frame are quantised more coarsely, cheaper rows more finely; the row QP is the frame QP plus the
+ * offset, clipped to the frame's window (this project's rule; OpenH264 re-plans GOMs from the bits
+ * of the frame being coded, a serial dependency). */
 int h264o_rc_row_delta(int64_t row_bits, int64_t mean) {
     if (mean <= 0) return 0;
     if (row_bits > 2 * mean) return 2;
@@ -81,7 +126,25 @@ static void rc_plan_rows(H264OEnc *e) {
     int64_t sum = 0;
     for (int r = 0; r < e->mbh; r++) sum += e->rowbits[r];
     int64_t mean = sum / e->mbh;
-    for (int r = 0; r < e->mbh; r++) e->rowqp[r] = clip3(QP_MIN, QP_MAX, e->qp + h264o_rc_row_delta(e->rowbits[r], mean));
+    for (int r = 0; r < e->mbh; r++) e->rowqp[r] = h264o_rc_row_delta(e->rowbits[r], mean);
+}
+/* oracle RC constants for tests/test_oracle_golden.py (pinned against the h264.wasm fixture) */
+void h264o_rc_constants(int32_t out[8]) {
+    out[0] = RC_FPS; out[1] = QP_MIN; out[2] = QP_MAX; out[3] = FRAME_DQP_LOWER; out[4] = FRAME_DQP_UPPER;
+    out[5] = IDR_QP_WINDOW; out[6] = 400; out[7] = 50;
+}
+/* the oracle's copy of an OpenH264 table, for the same test: returns the entry count (-1: unknown) */
+int h264o_table(const char *name, double *out) {
+    int n = 0;
+    if (!strcmp(name, "quant_mf")) { for (int i = 0; i < 52 * 8; i++) out[n++] = OH_QUANT_MF[i / 8][i % 8]; }
+    else if (!strcmp(name, "quant_ff")) { for (int i = 0; i < 58 * 8; i++) out[n++] = OH_QUANT_FF[i / 8][i % 8]; }
+    else if (!strcmp(name, "lambda")) { for (int i = 0; i < 52; i++) out[n++] = LAMBDA[i]; }
+    else if (!strcmp(name, "rc_bpp")) { for (int i = 0; i < 16; i++) out[n++] = OH_RC_BPP[i / 4][i % 4]; }
+    else if (!strcmp(name, "rc_init_qp")) { for (int i = 0; i < 20; i++) out[n++] = OH_RC_INIT_QP[i / 5][i % 5]; }
+    else if (!strcmp(name, "rc_qp_range")) { for (int i = 0; i < 10; i++) out[n++] = OH_RC_QP_RANGE[i / 2][i % 2]; }
+    else if (!strcmp(name, "rc_qstep")) { for (int i = 0; i < 52; i++) out[n++] = OH_RC_QSTEP[i]; }
+    else return -1;
+    return n;
 }
 /* mb_qp_delta carrying QP a from QP_pred b, wrapped into -26..25 (7.4.5) */
 static int qp_delta_wrap(int a, int b) { return ((a - b + 26 + 52) % 52) - 26; }
@@ -91,7 +154,7 @@ static int level_idc_for(int mbs) {
                                {31, 3600, 108000}, {32, 5120, 216000}, {40, 8192, 245760},  {42, 8704, 522240},
                                {50, 22080, 589824}, {51, 36864, 983040}, {52, 36864, 2073600}};
     for (unsigned i = 0; i < sizeof(L) / sizeof(L[0]); i++)
-        if (L[i][1] >= mbs && L[i][2] >= mbs * RC_FPS) return L[i][0];
+        if (L[i][1] >= mbs && L[i][2] >= mbs * LEVEL_FPS) return L[i][0];
     return 52;
 }
 
@@ -213,15 +276,6 @@ static int luma_block_levels(const uint8_t *src, int ss, const uint8_t *pred, in
     for (int k = first; k < 16; k++) lv[k] = (int16_t)quant4(c[ZIGZAG4[k]], qp, ZIGZAG4[k], intra);
     return c[0];
 }
-/* DC quantisation for luma DC (4x4 Hadamard, >>1) and chroma DC (2x2): (|f|*MF0 + 2f) >> (qbits+1) */
-static int quant_dc(int v, int qp, int intra) {
-    int qbits = 15 + qp / 6;
-    int f = (1 << qbits) / (intra ? 3 : 6);
-    int a = iabs(v);
-    int l = (int)(((int64_t)a * QUANT_MF[qp % 6][0] + 2 * f) >> (qbits + 1));
-    return v < 0 ? -l : l;
-}
-
 /* Chroma residual for one MB: levels + recon into rec planes. pred[pl][64]. */
 static void encode_chroma(H264OEnc *e, MBInfo *mb, int mbx, int mby, uint8_t pred[2][64], int intra) {
     int qpc = CHROMA_QP[mb->qp];
@@ -236,8 +290,8 @@ static void encode_chroma(H264OEnc *e, MBInfo *mb, int mbx, int mby, uint8_t pre
         }
         int f0 = dcraw[0] + dcraw[1] + dcraw[2] + dcraw[3], f1 = dcraw[0] - dcraw[1] + dcraw[2] - dcraw[3];
         int f2 = dcraw[0] + dcraw[1] - dcraw[2] - dcraw[3], f3 = dcraw[0] - dcraw[1] - dcraw[2] + dcraw[3];
-        mb->cdc[pl][0] = (int16_t)quant_dc(f0, qpc, intra); mb->cdc[pl][1] = (int16_t)quant_dc(f1, qpc, intra);
-        mb->cdc[pl][2] = (int16_t)quant_dc(f2, qpc, intra); mb->cdc[pl][3] = (int16_t)quant_dc(f3, qpc, intra);
+        mb->cdc[pl][0] = (int16_t)quant_dc4(f0, qpc, intra); mb->cdc[pl][1] = (int16_t)quant_dc4(f1, qpc, intra);
+        mb->cdc[pl][2] = (int16_t)quant_dc4(f2, qpc, intra); mb->cdc[pl][3] = (int16_t)quant_dc4(f3, qpc, intra);
         if (count_nz(mb->cdc[pl], 4)) any_dc = 1;
     }
     int cbpc = any_ac ? 2 : (any_dc ? 1 : 0);
@@ -302,7 +356,8 @@ static void encode_i16(H264OEnc *e, MBInfo *mb, int mbx, int mby, int mode, cons
         dcraw[ras] = luma_block_levels(src + oy * e->cw + ox, e->cw, pred + oy * 16 + ox, 16, qp, 1, 1, mb->luma[ras]);
         if (count_nz(mb->luma[ras], 16)) any_ac = 1;
     }
-    /* forward 4x4 Hadamard on the spatial DC matrix, then >> 1 */
+    /* forward 4x4 Hadamard on the spatial DC matrix, then (x + 1) >> 1 (WelsHadamardT4Dc, wasm func 1029;
+     * the int16 clip there never binds for 8-bit input: |x| <= 32640) */
     int t[16], f[16];
     for (int i = 0; i < 4; i++) {
         int a = dcraw[4 * i], b = dcraw[4 * i + 1], c = dcraw[4 * i + 2], d = dcraw[4 * i + 3];
@@ -310,9 +365,10 @@ static void encode_i16(H264OEnc *e, MBInfo *mb, int mbx, int mby, int mode, cons
     }
     for (int j = 0; j < 4; j++) {
         int a = t[j], b = t[4 + j], c = t[8 + j], d = t[12 + j];
-        f[j] = (a + b + c + d) >> 1; f[4 + j] = (a + b - c - d) >> 1; f[8 + j] = (a - b - c + d) >> 1; f[12 + j] = (a - b + c - d) >> 1;
+        f[j] = (a + b + c + d + 1) >> 1; f[4 + j] = (a + b - c - d + 1) >> 1; f[8 + j] = (a - b - c + d + 1) >> 1;
+        f[12 + j] = (a - b + c - d + 1) >> 1;
     }
-    for (int k = 0; k < 16; k++) mb->lumadc[k] = (int16_t)quant_dc(f[ZIGZAG4[k]], qp, 1);
+    for (int k = 0; k < 16; k++) mb->lumadc[k] = (int16_t)quant_dc4(f[ZIGZAG4[k]], qp, 1);
     mb->cbp = any_ac ? 15 : 0;
     int dc[16];
     luma_dc_dequant(mb->lumadc, qp, dc);
@@ -600,8 +656,8 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
     e->rowbits = (int64_t *)calloc((size_t)e->mbh, sizeof(int64_t));
     e->first = 1;
     e->skip_en = 1;  /* the wrapper leaves OpenH264's frame skipping on (bEnableFrameSkip default) */
-    e->qp = h264o_rc_init_qp(w, h, bitrate);
-    rc_plan_rows(e);
+    e->init_qp = h264o_rc_idr_params(w, h, bitrate, &e->rmin, &e->rmax);
+    e->qp = e->init_qp;
     e->idr_pic_id = -1;
     return e;
 }
@@ -646,7 +702,7 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     load_source(e, yuv);
     e->first = 0; e->force_idr = 0;
     if (idr) { e->frame_num = 0; e->poc = 0; e->idr_pic_id = (e->idr_pic_id + 1) & 0xffff; }
-    int qp = e->qp;
+    int qp = rc_frame_qp(e, idr);
     size_t o = 0;
     uint8_t *tmp = (uint8_t *)malloc(64 + (size_t)e->cw * e->ch * 4);
     if (idr) { o += h264o_write_sps(e->w, e->h, tmp + o); o += h264o_write_pps(tmp + o); }
@@ -667,7 +723,7 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
      * QPY is the running QP (7.4.5) */
     int skip_run = 0, running = qp;
     for (int mby = 0; mby < e->mbh; mby++) {
-        const int qrow = e->rowqp[mby];
+        const int qrow = clip3(e->qmin, e->qmax, qp + e->rowqp[mby]);
         e->rowbits[mby] = 0;
         for (int mbx = 0; mbx < e->mbw; mbx++) {
             MBInfo *mb = &e->mbs[mby * e->mbw + mbx];

@@ -1,6 +1,7 @@
 """GPU: the device-resident batch API (many streams per launch, NAL units and sizes in HBM,
 frame-batched decoding) -- decoder picture == encoder reconstruction for every stream, stream
-bytes == oracle bytes, at the bench configuration's full 1080p size."""
+bytes == oracle bytes for EVERY stream of the launch (each against its own oracle encoder), at the bench
+configuration's full 1080p size."""
 import os
 import sys
 
@@ -20,7 +21,8 @@ sys.path.insert(0, os.path.join(ROOT, 'tools'))
     (1920, 1080, 1000000, 4, 6, 1, 3),   # bench geometry
     (352, 288, 2000000, 3, 9, 1, 3, 16),    # reserved decode lane: parse on 16 masked CUs, wavefronts on the rest
     (1920, 1080, 1000000, 4, 6, 1, 2, 16),  # the same at the bench geometry
-], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3', 'cif-lanes16', '1080p-lanes16'])
+    (1920, 1080, 1000000, 32, 3, 1, 3, 32),  # the bench's own launch: 32 streams, 32 parse CUs, every stream vs its oracle
+], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3', 'cif-lanes16', '1080p-lanes16', '1080p-s32-lanes32'])
 def test_batch_encode_decode(gpu_lib, args):
     import batch_check
     assert batch_check.main(*args)

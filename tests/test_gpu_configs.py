@@ -58,21 +58,22 @@ def _run_capi(L, oracle, w, h, br, nf, i_only, sid=0):
     return sizes, qps
 
 
-def test_config3_1080p_ippp_8mbps_30_frames(gpu_lib, oracle):
-    """configs[2] at 8 Mbps, the non-degenerate operating point: 1 IDR + 29 P frames (frame skipping on,
-    as the wrapper's encoder), every frame coded with real residuals (QP in the 30s), NAL bytes and
-    decoded pictures == oracle frame by frame"""
-    sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 8000000, 30, False)
-    assert sum(1 for n in sizes[1:] if n > 0) >= 25, sizes  # P frames really coded
-    assert max(qps[1:]) < 45, qps                            # not the QP-51 collapse regime
+def test_config3_1080p_ippp_8mbps_60_frames(gpu_lib, oracle):
+    """configs[2] at its stated span (60 frames IPPP, 1 IDR + 59 P) at 8 Mbps (frame
+    skipping on, as the wrapper's encoder): NAL bytes and decoded pictures == oracle frame by frame, with
+    the QP inside OpenH264's camera range [12, 42] and the IDR at the table QP"""
+    sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 8000000, 60, False)
+    assert sum(1 for n in sizes[1:] if n > 0) >= 40, sizes  # P frames really coded
+    assert qps[0] == 30 and max(qps) <= 42, qps
 
 
 def test_config3_1080p_ippp_1mbps_rc_skipping(gpu_lib, oracle):
     """configs[2] at the glue's 1 Mbps with the wrapper's frame skipping: the rate control drops the
     frames its buffer cannot take (0-byte access units) -- GPU == oracle, including which
     frames are skipped; every coded frame decodes to the oracle's picture"""
-    sizes, _ = _run_capi(gpu_lib, oracle, 1920, 1080, 1000000, 12, False)
+    sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 1000000, 12, False)
     assert sizes[0] > 0 and 0 in sizes[1:], sizes
+    assert qps[0] == 36, qps  # RcCalculateIdrQp at 1 Mbps, 60 fps default: bpp 0.008 -> QP 36 in [28, 40]
 
 
 @pytest.mark.parametrize('br', [1000000, 8000000], ids=['1mbps', '8mbps'])

@@ -212,10 +212,13 @@ def test_ring_wraps_without_host_sync(gpu_lib):
     enc.close()
 
 
-def test_ring_failed_frame_publishes_nothing(gpu_lib, oracle):
-    """A frame whose kernels fail (injected as an RBSP overflow) publishes nothing to the ring -- no
-    truncated access unit reaches a consumer -- and the encoder restarts with an IDR (SPS + PPS + IDR
-    slice): the decoder, which never saw the failed frame, decodes the stream on."""
+@pytest.mark.parametrize('code', [2, 3], ids=['after-assembly', 'rbsp-overflow-branch'])
+def test_ring_failed_frame_publishes_nothing(gpu_lib, oracle, code):
+    """A frame whose kernels fail publishes nothing to the ring -- no truncated or stale access unit
+    reaches a consumer -- and the encoder restarts with an IDR (SPS + PPS + IDR slice): the decoder,
+    which never saw the failed frame, decodes the stream on. Code 2 fails the frame after
+    the slice is assembled; code 3 takes enc_pack_kernel's RBSP-overflow early exit itself (ADVICE r3:
+    that exit used to leave the previous frame's size in place)."""
     import torch
     import h264mi
     w, h, n, bad = 176, 144, 5, 2
@@ -227,7 +230,7 @@ def test_ring_failed_frame_publishes_nothing(gpu_lib, oracle):
     od = oracle.decoder()
     for t in range(n):
         if t == bad:
-            enc.inject_error(0, 2)
+            enc.inject_error(0, code)
         enc.encode(frames[t])
         tk = ring.publish(enc, 0, 1)
         torch.cuda.synchronize()

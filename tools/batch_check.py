@@ -1,8 +1,8 @@
 """Debug driver for the batch (device-resident) API: S streams encoded by BatchEncoder and decoded by
 BatchDecoder. With group G = 1 every frame is decoded right after it is encoded (decode or
 decode_dev); with G > 1 frames are staged and decoded G at a time (decode_frames). Checks per
-decode call: decoder status, decoder picture == encoder reconstruction (every stream), and stream
-0's bytes == oracle bytes for every frame. lanes > 0: encoder and reconstruction on streams masked off
+decode call: decoder status, decoder picture == encoder reconstruction (every stream), and EVERY
+stream's bytes == the bytes of that stream's own oracle encoder (seed s) for every frame. lanes > 0: encoder and reconstruction on streams masked off
 CU bits [0, lanes), entropy decoding (4 parse streams) on those CUs -- the bench's reserved decode lane.
 usage: batch_check.py w h br S nf [dev=1] [G=1] [lanes=0]"""
 import ctypes, os, sys
@@ -17,8 +17,9 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0):
     from h264mi.synth import SyntheticStream
     O = ctypes.CDLL(os.path.join(ROOT, 'oracle/build/libh264_oracle.so'))
     O.h264o_enc_create.restype = ctypes.c_void_p
-    oe = ctypes.c_void_p(O.h264o_enc_create(w, h, br))
-    O.h264o_enc_set_frame_skip(oe, 0)  # the batch pipeline under test decodes every frame
+    oes = [ctypes.c_void_p(O.h264o_enc_create(w, h, br)) for _ in range(S)]  # one oracle encoder per stream
+    for oe in oes:
+        O.h264o_enc_set_frame_skip(oe, 0)  # the batch pipeline under test decodes every frame
     F = w * h * 3 // 2
     gens = [SyntheticStream(s, w, h) for s in range(S)]
     st = h264mi.masked_stream(0, lanes, True) if lanes else None
@@ -36,15 +37,17 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0):
     t = 0
     while t < nf:
         n = min(G, nf - t)
-        same0 = True
+        same = [True] * S
         sizes = None
         for j in range(n):
             host = np.concatenate([g.frame(t + j) for g in gens])
             with torch.cuda.stream(st) if st is not None else torch.cuda.stream(torch.cuda.current_stream()):
                 enc.encode(torch.from_numpy(host).cuda())
             sizes = enc.nal_sizes()
-            m = O.h264o_enc_encode(oe, host[:F].ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(out.size))
-            same0 = same0 and enc.nal_bytes(0, sizes[0]) == out[:m].tobytes()
+            for s, oe in enumerate(oes):
+                m = O.h264o_enc_encode(oe, host[s * F:(s + 1) * F].ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.c_int(out.size))
+                same[s] = same[s] and enc.nal_bytes(s, sizes[s]) == out[:m].tobytes()
             if G > 1:
                 enc.copy_nals(stage[j], slot, stage_sz[j])
         if G == 1:
@@ -75,10 +78,12 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0):
                 d = np.nonzero(a != b)[0]
                 print('   stream0 first diff', d[0], 'count', len(d), 'luma' if d[0] < cw * ch else 'chroma',
                       (d[0] % cw, d[0] // cw) if d[0] < cw * ch else '')
-        print(f'frames {t}..{t + n - 1}: last sizes {sizes} oracle-bytes-equal(stream0)={same0} dec rc={rc} got={got} '
+        print(f'frames {t}..{t + n - 1}: last sizes {sizes} oracle-bytes-equal(every stream)={same} dec rc={rc} got={got} '
               f'recon==dec {eq}', flush=True)
-        ok = ok and same0 and rc == 0 and all(got) and all(eq)
+        ok = ok and all(same) and rc == 0 and all(got) and all(eq)
         t += n
+    for oe in oes:
+        O.h264o_enc_destroy(oe)
     return ok
 
 

@@ -7,8 +7,10 @@ Modes (what one timed frame is, matching bench.py's configs):
   encdec  1 IDR untimed, then P frames encoded + decoded        (metric, configs 3 and 5)
   enc_i   every frame forced IDR, encoded                         (config 2)
   dec     the stream is encoded untimed, then its P frames decoded (config 4)
-Also (--hash K): sha256 of the oracle's NAL bytes and decoded pictures of stream 0's first K frames,
-which bench.py compares with the GPU's bytes for the same frames (parity at the bench's own size).
+Also (--hash K): sha256 of the oracle's NAL bytes and decoded pictures of the first K frames of stream 0
+-- or, with --hash-streams N, of each of streams F..F+N-1 (--hash-first F; one oracle encoder and decoder
+per stream, in parallel worker processes) -- which bench.py compares with the bytes and pictures of the
+timed pipeline's own streams (parity at the bench's own size and stream count).
 Run as a child process before the parent touches the GPU.
 """
 import argparse, ctypes, hashlib, json, os, sys, time
@@ -118,9 +120,19 @@ def main():
     ap.add_argument('--hash', type=int, default=0, help='sha256 of stream 0 frames 0..K-1 (NAL bytes, decoded picture)')
     ap.add_argument('--hash-stream', type=int, default=0, help='synthetic stream id whose frames are hashed')
     ap.add_argument('--hash-only', action='store_true', help='only the parity hashes (no timing; N > 1 ranks)')
+    ap.add_argument('--hash-streams', type=int, default=0, help='hash the first K frames of N streams (--hash-first ..)')
+    ap.add_argument('--hash-first', type=int, default=0, help='first synthetic stream id of --hash-streams')
     a = ap.parse_args()
     allc = a.procs or host_cores()
+    streams_hashes = None
+    if a.hash_streams > 0 and a.hash > 0:
+        jobs = [(sid, a.width, a.height, a.bitrate, a.hash, a.mode, a.hash) for sid in range(a.hash_first, a.hash_first + a.hash_streams)]
+        with mp.get_context('spawn').Pool(min(allc, len(jobs))) as pool:
+            streams_hashes = {str(j[0]): r[2] for j, r in zip(jobs, pool.map(worker, jobs))}
     if a.hash_only:
+        if streams_hashes is not None:
+            print(json.dumps({'parity_hashes_streams': streams_hashes}))
+            return
         _, _, hashes, _ = worker((a.hash_stream, a.width, a.height, a.bitrate, a.hash, a.mode, a.hash))
         print(json.dumps({'parity_hashes': hashes, 'stream': a.hash_stream}))
         return
@@ -131,7 +143,7 @@ def main():
          'build': 'oracle/build/libh264_oracle.so, gcc -O3 -march=x86-64-v3',
          'sample': f'{allc} procs x 1 stream x {a.frames} frames {a.width}x{a.height} at {a.bitrate} bps '
                    f'({what}; {nn} timed frames, slowest process {bn:.2f} s); 1-core: {n1} frames in {b1:.2f} s',
-         'wall_s': round(w1 + wn, 2), 'parity_hashes': hashes}
+         'wall_s': round(w1 + wn, 2), 'parity_hashes': hashes, 'parity_hashes_streams': streams_hashes}
     if a.mode == 'encdec':  # the encode share of the same timed frames (north_star: "host-CPU encode FPS")
         d['encode_only'] = {'value': en, 'value_1core': e1, 'unit': 'frames/s', 'cores': allc,
                             'sample': 'encode calls of the same timed P frames (decode time excluded)'}

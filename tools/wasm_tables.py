@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Read OpenH264's encoder constants out of the reference's prebuilt scripts/h264.wasm AS BYTES.
+
+The module is never instantiated, translated to something runnable or linked: this script parses the
+binary's section headers, maps its passive data segments to linear-memory addresses (the start
+function's `i32.const dest; i32.const 0; i32.const size; memory.init seg` sequence, read as a byte
+pattern), copies tables out of the data segments, and decodes the immediate operand of a handful of
+individual instructions at known file offsets. Nothing is executed.
+
+What it pins: the wrapper links cisco/openh264 (not vendored, no tag),
+so these constants are the only part of OpenH264's encoder arithmetic the reference itself holds:
+
+  tables   quantiser MF (int16[52][8]), quantiser rounding FF (int16[58][8]; intra = row qp + 6),
+           lambda (int32[52]), rate-control bits-per-pixel thresholds (f64[4][4]), initial IDR QP
+           (int32[4][5]), IDR QP range (int32[5][2]), QP -> Qstep (int32[52])
+  code     the immediates the RC control flow around those tables uses (camera-content QP limits,
+           the default frame rate, the frame-to-frame QP window, ...), each at the file offset of
+           the instruction that carries it, with the function it sits in
+
+Where each fact was found (wasm function indices count imports; offsets are file offsets):
+  func 1226  WelsRcPictureInitGom with RcCalculateIdrQp / RcCalculatePictureQp inlined
+             (bpp search 767012-767140, QP range 767141-767222, initial QP 767244, frame window
+             767530/767559, P-frame window 768096-768207)
+  func  592  RcInitSequenceParameter (iFrameDeltaQpLower/Upper 401384-401409, skip ratio 401267)
+  func  597  parameter validation (iMinQp/iMaxQp defaults 408923-409035)
+  func 1023  GetDefaultParams (fMaxFrameRate 690465, bFixRCOverShoot 690589, iIdrBitrateRatio 690580)
+  func 1029  WelsHadamardT4Dc: luma DC Hadamard (x + 1) >> 1 with int16 clip (691446-691537)
+  funcs 265/345/534/536  quantiser callers: DC quantised with (int16)(FF[0] << 1), MF[0] >> 1; intra
+             rows at FF + 6 rows (345 @190274 load16_u off=96, 536 @283180 i32.const 38992)
+
+  python tools/wasm_tables.py [--wasm PATH] [--out tests/golden/openh264_tables.json]
+"""
+import argparse
+import hashlib
+import json
+import os
+import re
+import struct
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+DEFAULT_WASM = '/root/reference/scripts/h264.wasm'
+DEFAULT_OUT = os.path.join(ROOT, 'tests', 'golden', 'openh264_tables.json')
+
+
+def uleb(b, i):
+    r = s = 0
+    while True:
+        x = b[i]
+        i += 1
+        r |= (x & 0x7f) << s
+        s += 7
+        if x < 0x80:
+            return r, i
+
+
+def sleb(b, i):
+    r = s = 0
+    while True:
+        x = b[i]
+        i += 1
+        r |= (x & 0x7f) << s
+        s += 7
+        if x < 0x80:
+            if x & 0x40:
+                r -= 1 << s
+            return r, i
+
+
+def sections(b):
+    assert b[:8] == b'\x00asm\x01\x00\x00\x00', 'not a wasm v1 module'
+    out, i = {}, 8
+    while i < len(b):
+        sid = b[i]
+        n, i = uleb(b, i + 1)
+        out[sid] = (i, n)
+        i += n
+    return out
+
+
+def data_segments(b, secs):
+    """[(file offset, size)] of the data section's segments (all passive in this module)."""
+    i, _ = secs[11]
+    cnt, i = uleb(b, i)
+    segs = []
+    for _ in range(cnt):
+        flag, i = uleb(b, i)
+        if flag == 0:  # active: i32.const expr
+            assert b[i] == 0x41
+            _, i = sleb(b, i + 1)
+            assert b[i] == 0x0b
+            i += 1
+        elif flag != 1:
+            raise ValueError(f'unsupported data segment flag {flag}')
+        sz, i = uleb(b, i)
+        segs.append((i, sz))
+        i += sz
+    return segs
+
+
+MEMORY_INIT = re.compile(rb'\x41([\x80-\xff]*[\x00-\x7f])\x41\x00\x41([\x80-\xff]*[\x00-\x7f])\xfc\x08(.)\x00', re.S)
+
+
+def segment_addresses(b, secs, segs):
+    """linear-memory address of each passive segment, from the memory.init sequence of the start
+    function (a byte pattern inside the code section: dest, source offset 0, size, seg)."""
+    c0, n = secs[10]
+    addr = {}
+    for m in MEMORY_INIT.finditer(b, c0, c0 + n):
+        dest, _ = sleb(m.group(1) + b'\x00', 0)
+        size, _ = sleb(m.group(2) + b'\x00', 0)
+        k = m.group(3)[0]
+        if k < len(segs) and segs[k][1] == size and k not in addr:
+            addr[k] = dest
+    if len(addr) != len(segs):
+        raise ValueError(f'mapped {len(addr)} of {len(segs)} segments')
+    return addr
+
+
+class Memory:
+    """read-only view of the initial linear memory image the data segments describe"""
+
+    def __init__(self, b):
+        self.b = b
+        self.secs = sections(b)
+        self.segs = data_segments(b, self.secs)
+        self.addr = segment_addresses(b, self.secs, self.segs)
+
+    def file_offset(self, mem, nbytes):
+        for k, (fo, sz) in enumerate(self.segs):
+            a = self.addr[k]
+            if a <= mem and mem + nbytes <= a + sz:
+                return fo + (mem - a)
+        raise ValueError(f'address {mem} (+{nbytes}) is not inside one data segment')
+
+    def read(self, mem, fmt, count):
+        n = struct.calcsize('<' + fmt) * count
+        fo = self.file_offset(mem, n)
+        return list(struct.unpack_from(f'<{count}{fmt}', self.b, fo)), fo
+
+
+# name: (linear-memory address, struct format, shape, meaning)
+TABLES = {
+    'quant_ff': (38896, 'h', (58, 8), 'g_kiQuantInterFF: rounding offset per (qp, position); inter rows qp, intra rows qp + 6'),
+    'quant_mf': (39824, 'h', (52, 8), 'g_kiQuantMF: level = ((|x| + FF) * MF) >> 16; DC: ((|x| + (FF[0] << 1)) * (MF[0] >> 1)) >> 16'),
+    'lambda': (40768, 'i', (52,), 'g_kiQpCostTable: motion / mode cost lambda per QP'),
+    'rc_bpp': (43440, 'd', (4, 4), 'RcCalculateIdrQp dBppArray[iBppIndex][i], iBppIndex by luma area <= 28800 / 115200 / 460800 / else'),
+    'rc_init_qp': (43568, 'i', (4, 5), 'RcCalculateIdrQp initial IDR QP [iBppIndex][i]'),
+    'rc_qp_range': (43648, 'i', (5, 2), 'RcCalculateIdrQp {max, min} QP of the IDR [i]'),
+    'rc_qstep': (43696, 'i', (52,), 'g_kiQpToQstepTable (RcConvertQp2QStep): round(100 * 2^((qp - 4) / 6))'),
+}
+
+# name: (file offset of the instruction, opcode, function, meaning)
+CODE_CONSTANTS = {
+    'camera_min_qp': (408976, 'i32.const', 597, 'iMinQp when the caller leaves it 0 (camera content)'),
+    'camera_max_qp': (408980, 'i32.const', 597, 'iMaxQp when the caller leaves iMinQp 0 (camera content)'),
+    'screen_min_qp': (408923, 'i32.const', 597, 'iMinQp default for screen content (unused by the wrapper)'),
+    'screen_max_qp': (408927, 'i32.const', 597, 'iMaxQp default for screen content (unused by the wrapper)'),
+    'default_max_frame_rate': (690465, 'f32bits', 1023, 'GetDefaultParams fMaxFrameRate (the wrapper never sets it)'),
+    'default_fix_rc_overshoot': (690589, 'i32.const', 1023, 'GetDefaultParams bFixRCOverShoot: the IDR bpp search starts at column !flag'),
+    'default_idr_bitrate_ratio': (690580, 'i32.const', 1023, 'GetDefaultParams iIdrBitrateRatio (percent)'),
+    'frame_delta_qp_lower': (401392, 'i32.const', 592, 'iFrameDeltaQpLower = this - iRcVaryRatio / 100 (ratio 0 by default)'),
+    'frame_delta_qp_upper': (401406, 'i32.const', 592, 'iFrameDeltaQpUpper = this - iRcVaryRatio / 50'),
+    'skip_buffer_ratio': (401267, 'i32.const', 592, 'iSkipBufferRatio (percent of the bitrate the skip buffer holds)'),
+    'idr_frame_qp_window': (767530, 'i32.const', 1226, 'RcCalculateIdrQp iMaxFrameQp = clip(QP + this), iMinFrameQp = clip(QP - this)'),
+    'bits_exceeded_qp_step': (767701, 'i32.const', 1226, 'RcCalculatePictureQp: QP = last QP + this when the bits level is exceeded'),
+    'cmplx_ratio_hi': (767802, 'i64.const', 1226, 'complexity ratio clamp, high (INT_MULTIPLY 100 + FRAME_CMPLX_RATIO_RANGE)'),
+    'cmplx_ratio_lo': (767805, 'i64.const', 1226, 'complexity ratio clamp, low'),
+    'area_90p': (766979, 'i32.const', 1226, 'iBppIndex 0 when w * h < this (<= 28800)'),
+    'area_180p': (766991, 'i32.const', 1226, 'iBppIndex 1 when w * h < this'),
+    'area_360p': (767005, 'i32.const', 1226, 'iBppIndex 2 when w * h < this, else 3'),
+}
+
+
+def decode_const(b, off, op):
+    if op in ('i32.const', 'f32bits'):
+        assert b[off] == 0x41, f'no i32.const at {off}'
+        v, _ = sleb(b, off + 1)
+        if op == 'f32bits':
+            v = struct.unpack('<f', struct.pack('<i', v))[0]
+        return v
+    if op == 'i64.const':
+        assert b[off] == 0x42, f'no i64.const at {off}'
+        return sleb(b, off + 1)[0]
+    raise ValueError(op)
+
+
+def extract(path):
+    b = open(path, 'rb').read()
+    mem = Memory(b)
+    out = {'source': 'scripts/h264.wasm (reference, prebuilt OpenH264 + wrapper; parsed as bytes, never executed)',
+           'sha256': hashlib.sha256(b).hexdigest(), 'bytes': len(b), 'tables': {}, 'code_constants': {},
+           'segments': [{'file_offset': fo, 'size': sz, 'address': mem.addr[k]} for k, (fo, sz) in enumerate(mem.segs)]}
+    for name, (addr, fmt, shape, meaning) in TABLES.items():
+        n = 1
+        for d in shape:
+            n *= d
+        vals, fo = mem.read(addr, fmt, n)
+        if len(shape) == 2:
+            vals = [vals[r * shape[1]:(r + 1) * shape[1]] for r in range(shape[0])]
+        out['tables'][name] = {'address': addr, 'file_offset': fo, 'type': {'h': 'int16', 'i': 'int32', 'd': 'f64'}[fmt],
+                               'shape': list(shape), 'meaning': meaning, 'values': vals}
+    for name, (off, op, func, meaning) in CODE_CONSTANTS.items():
+        out['code_constants'][name] = {'file_offset': off, 'instruction': op.replace('f32bits', 'i32.const (f32 bits)'),
+                                       'function': func, 'meaning': meaning, 'value': decode_const(b, off, op)}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--wasm', default=DEFAULT_WASM)
+    ap.add_argument('--out', default=DEFAULT_OUT)
+    a = ap.parse_args()
+    d = extract(a.wasm)
+    with open(a.out, 'w') as f:
+        json.dump(d, f, indent=1)
+        f.write('\n')
+    t = d['tables']
+    print(f"wrote {a.out}: lambda[51]={t['lambda']['values'][51]} mf[0]={t['quant_mf']['values'][0]} "
+          f"ff[57]={t['quant_ff']['values'][57]} camera QP [{d['code_constants']['camera_min_qp']['value']}, "
+          f"{d['code_constants']['camera_max_qp']['value']}] fps {d['code_constants']['default_max_frame_rate']['value']}")
+
+
+if __name__ == '__main__':
+    main()
