@@ -123,6 +123,10 @@ int h264mi_dec_ring_groups(h264mi_decoder *d);  /* slot groups in the decoder's 
 /* number of HIP streams the entropy decoding of consecutive calls rotates over (default 3, 1..16):
    up to that many calls are entropy-decoded concurrently; synchronises the decoder */
 int h264mi_dec_set_parse_streams(h264mi_decoder *d, int nstreams);
+/* slice-data waves per picture (1..32, default 1; the C-ABI's decoder slots use 8): wave j of a picture
+   parses its slices j, j + k, ... -- the slices of a multi-slice picture are independent CAVLC chains
+   (7.4.3: no neighbour across a slice edge), so up to k of them are entropy-decoded concurrently */
+int h264mi_dec_set_slice_waves(h264mi_decoder *d, int k);
 /* entropy decoding on reserved CUs: the parse streams get the CU mask bits [cu_lo, cu_hi) (the runtime
    stripes mask bits over the XCDs); cu_lo == cu_hi removes the mask. Pair with wavefront streams from
    h264mi_stream_create_cus(cu_lo, cu_hi, 1) so that encoder / reconstruction workgroups stay off them. */

@@ -34,7 +34,7 @@ struct MbInfo {
     int16_t mvd[2];      // encoder P16x16 mvd
     uint8_t sub[4];      // decoder P8x8 sub_mb_type
     int16_t mv[16][2];   // raster 4x4, quarter-pel
-    int32_t pad2;
+    int32_t pad2;        // decoder: slice identity + loop-filter parameters (MB_SLICE_*); encoder 0
 };
 static_assert(sizeof(MbInfo) == 128, "MbInfo layout");
 
@@ -124,10 +124,11 @@ struct DecState {
     DecParams psb[2];      // header chain: call k's dec_hdr_kernel reads psb[k & 1], its last wave writes psb[~k & 1]
     int32_t has_ref;       // reconstruction-side: a reference picture exists
     int32_t got_pic;       // 1 if the frame being (or last) reconstructed produced a picture
-    int32_t dbk_idc;       // disable_deblocking_filter_idc of that frame
+    int32_t nonref;        // that picture is a non-reference picture (nal_ref_idc 0): it is output, the reference stays
     int32_t err;           // of the current/last frame: 3 = parse error, 2 = unsupported, 1 = wavefront abort
     uint32_t epoch;        // hand-off tag, +1 per reconstructed picture
-    int32_t parity;        // pic[parity] = last output picture = reference for the next P slice
+    int32_t parity;        // pic[parity] = the reference for the next P slice
+    int32_t outpar;        // pic[outpar] = the last output picture (parity, or parity ^ 1 after a non-reference one)
 };
 
 // One decode call processes up to G frames per stream. Entropy decoding of a frame does not depend
@@ -135,20 +136,39 @@ struct DecState {
 // reconstruction / deblocking passes then run frame by frame. Calls take G-slot groups of a ring of
 // frame slots in turn and parse on two alternating HIP streams, so the slice data of consecutive
 // calls is entropy-decoded concurrently while earlier calls reconstruct (runtime_dec.inc).
-#define H264MI_MAX_NALS 32
+#define H264MI_MAX_NALS 40
+#define H264MI_MAX_SLICES 32
 struct NalEnt { int32_t start, end, type; uint32_t stop; };  // header byte index, payload end, type, RBSP stop-bit index
+// One slice of a picture: dec_scan_kernel (nal), dec_hdr_kernel (header fields), dec_parse_kernel (ok, end_mb).
+// info: what every MB record of the slice carries in MbInfo dword 31 (MB_SLICE_* below).
+struct SliceEnt {
+    int32_t nal;           // index into DecFrame::e
+    int32_t first_mb;      // first_mb_in_slice
+    int32_t slt;           // slice_type % 5 (0 P, 2 I)
+    int32_t qp;            // SliceQPY
+    uint32_t data_pos;     // RBSP bit index of slice_data()
+    uint32_t info;         // first_mb | idc << 20 | (FilterOffsetA / 2 & 15) << 22 | (FilterOffsetB / 2 & 15) << 26
+    int32_t ok;            // slice data parsed without error
+    int32_t end_mb;        // one past its last macroblock
+};
 struct DecFrame {          // per (frame slot, stream): written by dec_scan_kernel, dec_hdr_kernel, dec_parse_kernel
     const uint8_t *nal;
-    int32_t nbytes, nnal, slice, err, got_pic, dbk_idc;
-    // slice header results (dec_hdr_kernel) for the slice-data pass
-    int32_t hdr_ok;        // parameter sets and slice header parsed, slice data to follow
-    int32_t slt;           // slice_type % 5 (0 P, 2 I)
-    int32_t qp, cqp;       // SliceQPY, chroma_qp_index_offset
-    uint32_t data_pos;     // RBSP bit index of slice_data()
-    int32_t pad_h[3];
-    DecParams ps;          // parameter sets in effect for this frame's slice (cropping for the output)
+    int32_t nbytes, nnal, nsl, err, got_pic, nonref;
+    int32_t hdr_ok;        // parameter sets and every slice header parsed, slice data to follow
+    int32_t anyp;          // some slice is a P slice (needs a reference)
+    int32_t cqp;           // chroma_qp_index_offset
+    int32_t pad_h[5];
+    DecParams ps;          // parameter sets in effect for this frame's slices (cropping for the output)
     NalEnt e[H264MI_MAX_NALS];
+    SliceEnt sl[H264MI_MAX_SLICES];
 };
+// MbInfo dword 31 (pad2) of a decoded MB: its slice's first MB (neighbour availability: a preceding MB
+// is in the same slice iff its address >= first) and loop-filter parameters (deblock.inc). 0 for the
+// encoder's single-slice pictures.
+#define MB_SLICE_FIRST(w) ((int)((w) & 0xFFFFFu))
+#define MB_SLICE_IDC(w) ((int)(((w) >> 20) & 3u))
+#define MB_SLICE_OFFA(w) (2 * (((int)((w) << 6)) >> 28))   // bits 22..25, signed, x2
+#define MB_SLICE_OFFB(w) (2 * (((int)((w) << 2)) >> 28))   // bits 26..29, signed, x2
 // one access unit; out / got (optional, device): where dec_output_kernel puts this frame's cropped tight
 // I420 picture and its got-picture flag once the frame is reconstructed (every frame of a batched call)
 struct DecInput { const uint8_t *nal; const int32_t *size_dev; int32_t size, pad; uint8_t *out; int32_t *got; };

@@ -79,6 +79,7 @@ def lib():
             'h264mi_dec_recon_profile': (i, [vp, vp]),
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_set_parse_streams': (i, [vp, i]),
+            'h264mi_dec_set_slice_waves': (i, [vp, i]),
             'h264mi_dec_set_parse_cus': (i, [vp, i, i]),
             'h264mi_stream_create_cus': (vp, [i, i, i]),
             'h264mi_stream_destroy': (None, [vp]),
@@ -403,6 +404,11 @@ class BatchDecoder:
         """entropy decoding on CU mask bits [lo, hi) (see h264mi_dec_set_parse_cus)"""
         if self._L.h264mi_dec_set_parse_cus(self._d, lo, hi) != 0:
             raise RuntimeError('h264mi_dec_set_parse_cus failed')
+
+    def set_slice_waves(self, k):
+        """slice-data waves per picture (h264mi_dec_set_slice_waves): a multi-slice picture's slices in parallel"""
+        if self._L.h264mi_dec_set_slice_waves(self._d, k) != 0:
+            raise RuntimeError('h264mi_dec_set_slice_waves failed')
 
     def set_parse_streams(self, n):
         if self._L.h264mi_dec_set_parse_streams(self._d, n) != 0:

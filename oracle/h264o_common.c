@@ -403,13 +403,12 @@ static NbMv nb_mv(const MBInfo *mbs, const MBInfo *cur, unsigned done_mask, int 
     const MBInfo *m;
     int nx, ny;
     if (y < 0) {
-        if (mby == 0) return r;
-        if (x < 0) { if (mbx == 0) return r; m = &mbs[(mby - 1) * mbw + mbx - 1]; nx = x + 16; }
-        else if (x < 16) { m = &mbs[(mby - 1) * mbw + mbx]; nx = x; }
-        else { if (mbx + 1 >= mbw) return r; m = &mbs[(mby - 1) * mbw + mbx + 1]; nx = x - 16; }
+        if (x < 0) { if (!mb_nb_avail(mbs, mbw, mbx, mby, -1, -1)) return r; m = &mbs[(mby - 1) * mbw + mbx - 1]; nx = x + 16; }
+        else if (x < 16) { if (!mb_nb_avail(mbs, mbw, mbx, mby, 0, -1)) return r; m = &mbs[(mby - 1) * mbw + mbx]; nx = x; }
+        else { if (!mb_nb_avail(mbs, mbw, mbx, mby, 1, -1)) return r; m = &mbs[(mby - 1) * mbw + mbx + 1]; nx = x - 16; }
         ny = y + 16;
     } else if (x < 0) {
-        if (mbx == 0) return r;
+        if (!mb_nb_avail(mbs, mbw, mbx, mby, -1, 0)) return r;
         m = &mbs[mby * mbw + mbx - 1]; nx = x + 16; ny = y;
     } else if (x >= 16) {
         return r;
@@ -463,9 +462,9 @@ void mvp_part(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, i
 /* 8.4.1.1 P_Skip motion vector */
 void pskip_mv(const MBInfo *mbs, int mbw, int mbx, int mby, int out[2]) {
     out[0] = out[1] = 0;
-    if (mbx == 0 || mby == 0) return;
     NbMv A = nb_mv(mbs, NULL, 0, mbw, mbx, mby, -1, 0);
     NbMv B = nb_mv(mbs, NULL, 0, mbw, mbx, mby, 0, -1);
+    if (!A.avail || !B.avail) return;  /* mbAddrA or mbAddrB not available: (0, 0) */
     if (A.ref == 0 && A.mv[0] == 0 && A.mv[1] == 0) return;
     if (B.ref == 0 && B.mv[0] == 0 && B.mv[1] == 0) return;
     mvp_16x16(mbs, mbw, mbx, mby, out);
@@ -520,26 +519,32 @@ static int compute_bs(const MBInfo *mp, int rp, const MBInfo *mq, int rq, int mb
     if (iabs(mp->mv[rp][0] - mq->mv[rq][0]) >= 4 || iabs(mp->mv[rp][1] - mq->mv[rq][1]) >= 4) return 1;
     return 0;
 }
-/* cqp_off: chroma_qp_index_offset (8.7.2.2: QPc of each MB from its QPY + offset; I_PCM QPY = 0);
- * off_a, off_b: FilterOffsetA/B = slice_alpha_c0_offset_div2 << 1, slice_beta_offset_div2 << 1 */
+/* cqp_off: chroma_qp_index_offset (8.7.2.2: QPc of each MB from its QPY + offset; I_PCM QPY = 0).
+ * Per MB q, its slice's parameters (8.7, 7.4.3): dbk_idc 1 -> q is not filtered; 2 -> its left / top
+ * MB edge is not filtered when the MB across it belongs to another slice; FilterOffsetA/B = dbk_a /
+ * dbk_b (slice_alpha_c0_offset_div2 << 1, slice_beta_offset_div2 << 1). */
 void deblock_frame(uint8_t *Y, uint8_t *U, uint8_t *V, int ys, int cs, const MBInfo *mbs, int mbw, int mbh,
-                   int cqp_off, int off_a, int off_b) {
+                   int cqp_off) {
     for (int my = 0; my < mbh; my++)
         for (int mx = 0; mx < mbw; mx++) {
             const MBInfo *q = &mbs[my * mbw + mx];
+            if (q->dbk_idc == 1) continue;
+            const int off_a = q->dbk_a, off_b = q->dbk_b;
+            const int left_ok = mx > 0 && (q->dbk_idc != 2 || mbs[my * mbw + mx - 1].slice_first == q->slice_first);
+            const int top_ok = my > 0 && (q->dbk_idc != 2 || mbs[(my - 1) * mbw + mx].slice_first == q->slice_first);
             int qpq = mb_qp_dbk(q), qcq = CHROMA_QP[clip3(0, 51, qpq + cqp_off)];
             int bs[2][4][4]; /* [dir][edge][segment] */
             for (int e = 0; e < 4; e++)
                 for (int s = 0; s < 4; s++) {
                     /* vertical edge e (x = 4e), segment s (rows 4s..4s+3) */
-                    if (e == 0) bs[0][0][s] = mx > 0 ? compute_bs(&mbs[my * mbw + mx - 1], s * 4 + 3, q, s * 4, 1) : 0;
+                    if (e == 0) bs[0][0][s] = left_ok ? compute_bs(&mbs[my * mbw + mx - 1], s * 4 + 3, q, s * 4, 1) : 0;
                     else bs[0][e][s] = compute_bs(q, s * 4 + e - 1, q, s * 4 + e, 0);
-                    if (e == 0) bs[1][0][s] = my > 0 ? compute_bs(&mbs[(my - 1) * mbw + mx], 12 + s, q, s, 1) : 0;
+                    if (e == 0) bs[1][0][s] = top_ok ? compute_bs(&mbs[(my - 1) * mbw + mx], 12 + s, q, s, 1) : 0;
                     else bs[1][e][s] = compute_bs(q, (e - 1) * 4 + s, q, e * 4 + s, 0);
                 }
             for (int dir = 0; dir < 2; dir++) {
                 for (int e = 0; e < 4; e++) {
-                    if (e == 0 && ((dir == 0 && mx == 0) || (dir == 1 && my == 0))) continue;
+                    if (e == 0 && ((dir == 0 && !left_ok) || (dir == 1 && !top_ok))) continue;
                     const MBInfo *p = e == 0 ? (dir == 0 ? &mbs[my * mbw + mx - 1] : &mbs[(my - 1) * mbw + mx]) : q;
                     int qpp = mb_qp_dbk(p);
                     int qpav = (qpp + qpq + 1) >> 1;
@@ -574,8 +579,8 @@ void deblock_frame(uint8_t *Y, uint8_t *U, uint8_t *V, int ys, int cs, const MBI
 /* ================= CAVLC (9.2) ================= */
 int nc_luma(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, int ras) {
     int bx = ras & 3, by = ras >> 2, na = -1, nb = -1;
-    if (bx > 0) na = cur->nnz[ras - 1]; else if (mbx > 0) na = mbs[mby * mbw + mbx - 1].nnz[ras + 3];
-    if (by > 0) nb = cur->nnz[ras - 4]; else if (mby > 0) nb = mbs[(mby - 1) * mbw + mbx].nnz[ras + 12];
+    if (bx > 0) na = cur->nnz[ras - 1]; else if (mb_nb_avail(mbs, mbw, mbx, mby, -1, 0)) na = mbs[mby * mbw + mbx - 1].nnz[ras + 3];
+    if (by > 0) nb = cur->nnz[ras - 4]; else if (mb_nb_avail(mbs, mbw, mbx, mby, 0, -1)) nb = mbs[(mby - 1) * mbw + mbx].nnz[ras + 12];
     if (na >= 0 && nb >= 0) return (na + nb + 1) >> 1;
     if (na >= 0) return na;
     if (nb >= 0) return nb;
@@ -583,8 +588,8 @@ int nc_luma(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, int
 }
 int nc_chroma(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, int pl, int blk) {
     int base = 16 + 4 * pl, bx = blk & 1, by = blk >> 1, na = -1, nb = -1;
-    if (bx > 0) na = cur->nnz[base + blk - 1]; else if (mbx > 0) na = mbs[mby * mbw + mbx - 1].nnz[base + blk + 1];
-    if (by > 0) nb = cur->nnz[base + blk - 2]; else if (mby > 0) nb = mbs[(mby - 1) * mbw + mbx].nnz[base + blk + 2];
+    if (bx > 0) na = cur->nnz[base + blk - 1]; else if (mb_nb_avail(mbs, mbw, mbx, mby, -1, 0)) na = mbs[mby * mbw + mbx - 1].nnz[base + blk + 1];
+    if (by > 0) nb = cur->nnz[base + blk - 2]; else if (mb_nb_avail(mbs, mbw, mbx, mby, 0, -1)) nb = mbs[(mby - 1) * mbw + mbx].nnz[base + blk + 2];
     if (na >= 0 && nb >= 0) return (na + nb + 1) >> 1;
     if (na >= 0) return na;
     if (nb >= 0) return nb;

@@ -42,7 +42,18 @@ typedef struct {
     uint8_t pcm[384];          /* I_PCM samples (decoder) */
     int8_t sub_type[4];        /* P8x8 sub_mb_type (decoder) */
     uint16_t done4;            /* decoder: 4x4 blocks whose motion is already derived (MV pred availability) */
+    int32_t slice_first;       /* first_mb_in_slice of the MB's slice (0: single-slice pictures, the encoder) */
+    int8_t dbk_idc, dbk_a, dbk_b; /* its slice's disable_deblocking_filter_idc, FilterOffsetA / B */
 } MBInfo;
+
+/* Neighbour MB (mbx + dx, mby + dy) of MB (mbx, mby), dy <= 0: available (6.4.8 / 6.4.9) when it is
+ * inside the picture and in the same slice. Slices are raster runs (no FMO), so a preceding MB is in
+ * the current slice exactly when its address is >= the slice's first_mb_in_slice. */
+static inline int mb_nb_avail(const MBInfo *mbs, int mbw, int mbx, int mby, int dx, int dy) {
+    const int x = mbx + dx, y = mby + dy;
+    if (x < 0 || y < 0 || x >= mbw) return 0;
+    return y * mbw + x >= mbs[mby * mbw + mbx].slice_first;
+}
 
 /* ---------------- bit writer (MSB first) ---------------- */
 typedef struct { uint8_t *buf; size_t cap, len; uint64_t acc; int nacc; } BW;
@@ -104,7 +115,7 @@ void mvp_part(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, i
 
 /* ---------------- deblocking ---------------- */
 void deblock_frame(uint8_t *y, uint8_t *u, uint8_t *v, int stride, int cstride, const MBInfo *mbs, int mbw, int mbh,
-                  int cqp_off, int off_a, int off_b);   /* 8.7 */
+                  int cqp_off);   /* 8.7; each MB with its slice's dbk_idc / dbk_a / dbk_b */
 
 /* ---------------- CAVLC ---------------- */
 int nc_luma(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, int ras);

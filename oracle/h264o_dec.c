@@ -4,9 +4,11 @@
  * CPU restatement of the decode path behind openh264_wrapper.cpp:253-280 (init_decoder) and
  * :424-464 (decode_frame_yuv_i420 -> ISVCDecoder::DecodeFrameNoDelay): the normative H.264
  * Baseline decoding process (clauses 7.3 syntax, 8.3 intra, 8.4 inter, 8.5 transform, 8.7 loop
- * filter, 9.2 CAVLC). Scope: CAVLC, frame MBs, one slice per picture, one reference frame,
- * all P partition shapes incl. sub-8x8, I_PCM. Out of scope (rejected with an error): FMO/ASO,
- * multiple slices per picture, more than one active reference, constrained intra prediction.
+ * filter, 9.2 CAVLC). Scope: CAVLC, frame MBs, any number of slices per picture in any order (ASO;
+ * I and P slices mixed in non-IDR pictures), neighbour availability and the loop filter's slice-edge
+ * rules per slice, non-reference pictures (decoded and output, the reference kept), one reference
+ * frame, all P partition shapes incl. sub-8x8, I_PCM. Out of scope (rejected with an error): FMO,
+ * more than one active reference, constrained intra prediction, redundant pictures.
  */
 #include "h264o_api.h"
 #include "h264o_common.h"
@@ -22,12 +24,15 @@ struct H264ODec {
     uint8_t *cur[3], *ref[3];
     int has_ref;
     MBInfo *mbs;
+    uint8_t *done;            /* per MB: decoded in the picture being assembled */
+    int pic_open, pic_idr, pic_ref;  /* the access unit's picture: started, IDR, nal_ref_idc != 0 */
 };
 
 H264ODec *h264o_dec_create(void) { return (H264ODec *)calloc(1, sizeof(H264ODec)); }
 static void free_frames(H264ODec *d) {
     for (int p = 0; p < 3; p++) { free(d->cur[p]); free(d->ref[p]); d->cur[p] = d->ref[p] = NULL; }
     free(d->mbs); d->mbs = NULL;
+    free(d->done); d->done = NULL;
 }
 void h264o_dec_destroy(H264ODec *d) { if (d) { free_frames(d); free(d); } }
 
@@ -62,6 +67,7 @@ static int parse_sps(H264ODec *d, BR *r) {
             d->cur[p] = (uint8_t *)calloc(n, 1); d->ref[p] = (uint8_t *)calloc(n, 1);
         }
         d->mbs = (MBInfo *)calloc((size_t)mbw * mbh, sizeof(MBInfo));
+        d->done = (uint8_t *)calloc((size_t)mbw * mbh, 1);
         d->has_ref = 0;
     }
     d->log2_mfn = log2_mfn; d->poc_type = poc_type; d->log2_poc = log2_poc; d->dpoaz = dpoaz;
@@ -89,26 +95,27 @@ static int parse_pps(H264ODec *d, BR *r) {
     return r->err ? -1 : 0;
 }
 
-static void nb16(const uint8_t *pl, int stride, int px, int py, int size, int has_top, int has_left, IntraNb *n) {
+static void nb16(const uint8_t *pl, int stride, int px, int py, int size, int has_top, int has_left, int has_tl, IntraNb *n) {
     memset(n, 0, sizeof(*n));
-    n->has_top = has_top; n->has_left = has_left; n->has_tl = has_top && has_left;
+    n->has_top = has_top; n->has_left = has_left; n->has_tl = has_tl;
     if (has_top) for (int i = 0; i < size; i++) n->top[i] = pl[(py - 1) * stride + px + i];
     if (has_left) for (int i = 0; i < size; i++) n->left[i] = pl[(py + i) * stride + px - 1];
     if (n->has_tl) n->tl = pl[(py - 1) * stride + px - 1];
 }
-static int tr_avail(int mbx, int mby, int mbw, int ras) {
+/* 4x4 block neighbours inside / across the macroblock (6.4.11.4), MBs by slice (mb_nb_avail) */
+static int tr_avail(const MBInfo *mbs, int mbx, int mby, int mbw, int ras) {
     int bx = ras & 3, by = ras >> 2;
-    if (by == 0) return bx < 3 ? mby > 0 : (mby > 0 && mbx + 1 < mbw);
+    if (by == 0) return mb_nb_avail(mbs, mbw, mbx, mby, bx < 3 ? 0 : 1, -1);
     if (bx == 3) return 0;
     return RAS2BLK[(by - 1) * 4 + bx + 1] < RAS2BLK[ras];
 }
-static void nb4(const uint8_t *pl, int stride, int mbx, int mby, int mbw, int ras, IntraNb *n) {
+static void nb4(const MBInfo *mbs, const uint8_t *pl, int stride, int mbx, int mby, int mbw, int ras, IntraNb *n) {
     int bx = ras & 3, by = ras >> 2, px = mbx * 16 + bx * 4, py = mby * 16 + by * 4;
     memset(n, 0, sizeof(*n));
-    n->has_top = by > 0 || mby > 0;
-    n->has_left = bx > 0 || mbx > 0;
-    n->has_tl = n->has_top && n->has_left;
-    n->has_tr = n->has_top && tr_avail(mbx, mby, mbw, ras);
+    n->has_top = by > 0 || mb_nb_avail(mbs, mbw, mbx, mby, 0, -1);
+    n->has_left = bx > 0 || mb_nb_avail(mbs, mbw, mbx, mby, -1, 0);
+    n->has_tl = (bx > 0 && by > 0) ? 1 : mb_nb_avail(mbs, mbw, mbx, mby, bx > 0 ? 0 : -1, by > 0 ? 0 : -1);
+    n->has_tr = n->has_top && tr_avail(mbs, mbx, mby, mbw, ras);
     if (n->has_top) {
         for (int i = 0; i < 4; i++) n->top[i] = pl[(py - 1) * stride + px + i];
         for (int i = 4; i < 8; i++) n->top[i] = n->has_tr ? pl[(py - 1) * stride + px + i] : n->top[3];
@@ -119,10 +126,10 @@ static void nb4(const uint8_t *pl, int stride, int mbx, int mby, int mbw, int ra
 static int pred_mode4(const MBInfo *mbs, const MBInfo *cur, int mbw, int mbx, int mby, int ras) {
     int bx = ras & 3, by = ras >> 2, a, b;
     if (bx > 0) a = cur->i4mode[ras - 1];
-    else if (mbx > 0) { const MBInfo *m = &mbs[mby * mbw + mbx - 1]; a = m->type == MBT_I4 ? m->i4mode[ras + 3] : 2; }
+    else if (mb_nb_avail(mbs, mbw, mbx, mby, -1, 0)) { const MBInfo *m = &mbs[mby * mbw + mbx - 1]; a = m->type == MBT_I4 ? m->i4mode[ras + 3] : 2; }
     else return 2;
     if (by > 0) b = cur->i4mode[ras - 4];
-    else if (mby > 0) { const MBInfo *m = &mbs[(mby - 1) * mbw + mbx]; b = m->type == MBT_I4 ? m->i4mode[ras + 12] : 2; }
+    else if (mb_nb_avail(mbs, mbw, mbx, mby, 0, -1)) { const MBInfo *m = &mbs[(mby - 1) * mbw + mbx]; b = m->type == MBT_I4 ? m->i4mode[ras + 12] : 2; }
     else return 2;
     return imin(a, b);
 }
@@ -176,14 +183,15 @@ static void recon_mb(H264ODec *d, MBInfo *mb, int mbx, int mby) {
             for (int blk = 0; blk < 16; blk++) {
                 int ras = BLK2RAS[blk], ox = (ras & 3) * 4, oy = (ras >> 2) * 4, coef[16];
                 IntraNb n; uint8_t p[16];
-                nb4(d->cur[0], ys, mbx, mby, d->mbw, ras, &n);
+                nb4(d->mbs, d->cur[0], ys, mbx, mby, d->mbw, ras, &n);
                 pred4x4(&n, mb->i4mode[ras], p);
                 dequant_block(mb->luma[ras], qp, 0, coef);
                 idct4_add(coef, Y + oy * ys + ox, ys, p, 4);
             }
         } else {
             IntraNb n; uint8_t p[256]; int dc[16];
-            nb16(d->cur[0], ys, mbx * 16, mby * 16, 16, mby > 0, mbx > 0, &n);
+            nb16(d->cur[0], ys, mbx * 16, mby * 16, 16, mb_nb_avail(d->mbs, d->mbw, mbx, mby, 0, -1),
+                 mb_nb_avail(d->mbs, d->mbw, mbx, mby, -1, 0), mb_nb_avail(d->mbs, d->mbw, mbx, mby, -1, -1), &n);
             pred16x16(&n, mb->i16mode, p);
             luma_dc_dequant(mb->lumadc, qp, dc);
             for (int ras = 0; ras < 16; ras++) {
@@ -195,7 +203,8 @@ static void recon_mb(H264ODec *d, MBInfo *mb, int mbx, int mby) {
         }
         for (int pl = 0; pl < 2; pl++) {
             IntraNb n;
-            nb16(d->cur[1 + pl], cs, mbx * 8, mby * 8, 8, mby > 0, mbx > 0, &n);
+            nb16(d->cur[1 + pl], cs, mbx * 8, mby * 8, 8, mb_nb_avail(d->mbs, d->mbw, mbx, mby, 0, -1),
+                 mb_nb_avail(d->mbs, d->mbw, mbx, mby, -1, 0), mb_nb_avail(d->mbs, d->mbw, mbx, mby, -1, -1), &n);
             pred_chroma(&n, mb->cmode, cpred[pl]);
         }
     } else {
@@ -235,16 +244,24 @@ static void set_part(MBInfo *mb, int bx, int by, int pw, int ph, const int mv[2]
         }
 }
 
+/* One slice of the access unit's picture (7.3.3, 7.3.4). The first slice opens the picture; the
+ * others must agree with it on IDR-ness and on being a reference picture (7.4.1.2.4). Returns 1 when
+ * the slice decoded, -1 on an error (the access unit is then concealed). */
 static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
     if (!d->have_sps || !d->have_pps) return -1;
-    /* a non-reference picture (nal_ref_idc 0) must not become the reference of the next P slice, and
-     * carries no dec_ref_pic_marking(); the wrapper's encoder never emits one: rejected (out of scope) */
-    if (nal_ref_idc == 0) return -1;
+    if (nal_type == 5 && nal_ref_idc == 0) return -1;
     int first_mb = br_ue(r);
     int st = br_ue(r) % 5;           /* 0 P, 2 I */
     br_ue(r);
-    if (first_mb != 0) return -1;     /* multiple slices per picture: out of scope */
+    const int total = d->mbw * d->mbh;
     if (st != 0 && st != 2) return -1;
+    if (first_mb >= total || (nal_type == 5 && st != 2)) return -1;
+    if (!d->pic_open) {
+        d->pic_open = 1; d->pic_idr = nal_type == 5; d->pic_ref = nal_ref_idc != 0;
+        memset(d->done, 0, (size_t)total);
+    } else if (d->pic_idr != (nal_type == 5) || d->pic_ref != (nal_ref_idc != 0)) {
+        return -1;
+    }
     br_get(r, d->log2_mfn);
     if (nal_type == 5) br_ue(r);
     if (d->poc_type == 0) { br_get(r, d->log2_poc); if (d->bottom_field_poc) br_se(r); }
@@ -260,15 +277,17 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
         if (!d->has_ref) return -1;
     }
     if (nref > 1 && st == 0) return -1;   /* multiple references: out of scope */
-    if (nal_type == 5) { br_get(r, 1); br_get(r, 1); }
-    else if (br_get(r, 1)) {
-        int op;
-        while ((op = br_ue(r)) != 0) {
-            if (op == 1 || op == 3) br_ue(r);
-            if (op == 2) br_ue(r);
-            if (op == 3 || op == 6) br_ue(r);
-            if (op == 4) br_ue(r);
-            if (r->err) return -1;
+    if (nal_ref_idc != 0) {               /* dec_ref_pic_marking() (7.3.3.3): reference pictures only */
+        if (nal_type == 5) { br_get(r, 1); br_get(r, 1); }
+        else if (br_get(r, 1)) {
+            int op;
+            while ((op = br_ue(r)) != 0) {
+                if (op == 1 || op == 3) br_ue(r);
+                if (op == 2) br_ue(r);
+                if (op == 3 || op == 6) br_ue(r);
+                if (op == 4) br_ue(r);
+                if (r->err) return -1;
+            }
         }
     }
     int qp = d->pic_init_qp + br_se(r);
@@ -282,7 +301,10 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
         }
     }
     if (r->err || qp < 0 || qp > 51 || d->cqp_off < -12 || d->cqp_off > 12) return -1;
-    int total = d->mbw * d->mbh, addr = 0, more = 1;
+    int addr = first_mb, more = 1;
+    /* every MB of the slice carries the slice's identity and loop-filter parameters */
+#define H264O_SLICE_MB(mb) do { (mb)->slice_first = first_mb; (mb)->dbk_idc = (int8_t)dbk_idc; (mb)->dbk_a = (int8_t)dbk_a; \
+                                (mb)->dbk_b = (int8_t)dbk_b; if (d->done[addr]) return -1; d->done[addr] = 1; } while (0)
     while (more && addr < total) {
         if (st == 0) {
             uint32_t run = br_ue(r);
@@ -291,6 +313,7 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
                 int mbx = addr % d->mbw, mby = addr / d->mbw;
                 MBInfo *mb = &d->mbs[addr];
                 memset(mb, 0, sizeof(*mb));
+                H264O_SLICE_MB(mb);
                 mb->type = MBT_PSKIP; mb->qp = qp;
                 for (int k = 0; k < 16; k++) mb->i4mode[k] = 2;
                 for (int k = 0; k < 4; k++) mb->ref[k] = 0;
@@ -305,6 +328,7 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
         int mbx = addr % d->mbw, mby = addr / d->mbw;
         MBInfo *mb = &d->mbs[addr];
         memset(mb, 0, sizeof(*mb));
+        H264O_SLICE_MB(mb);
         for (int k = 0; k < 16; k++) mb->i4mode[k] = 2;
         for (int k = 0; k < 4; k++) mb->ref[k] = -1;
         uint32_t mt = br_ue(r);
@@ -390,11 +414,8 @@ static int decode_slice(H264ODec *d, BR *r, int nal_type, int nal_ref_idc) {
         addr++;
         more = br_more_rbsp(r);
     }
-    if (addr != total) return -1;
-    /* per-picture loop filter with the slice's parameters */
-    /* idc 2 (no filtering across slice edges) equals idc 0 for the single slice per picture in scope */
-    if (dbk_idc != 1)
-        deblock_frame(d->cur[0], d->cur[1], d->cur[2], d->cw, d->cw / 2, d->mbs, d->mbw, d->mbh, d->cqp_off, dbk_a, dbk_b);
+#undef H264O_SLICE_MB
+    if (more && addr >= total && br_more_rbsp(r)) return -1;  /* slice data past the picture's end */
     return 1;
 }
 
@@ -415,6 +436,7 @@ int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out, i
     *w = *h = 0;
     if (!d || !data || size <= 0) return -1;
     int got_pic = 0, damaged = 0, i = 0;
+    d->pic_open = 0;
     while (i + 3 <= size) {
         /* find start code */
         int s = -1;
@@ -457,9 +479,20 @@ int h264o_dec_decode(H264ODec *d, const uint8_t *data, int size, uint8_t *out, i
         return 2;
     }
     if (!got_pic) return 0;
+    /* every macroblock of the picture decoded exactly once (its slices in any order), else concealed */
+    for (int k = 0; k < d->mbw * d->mbh; k++)
+        if (!d->done[k]) {
+            if (!d->has_ref) return -1;
+            emit_picture(d, d->ref, out, w, h);
+            return 2;
+        }
+    /* the loop filter over the whole picture, each MB with its slice's parameters (8.7) */
+    deblock_frame(d->cur[0], d->cur[1], d->cur[2], d->cw, d->cw / 2, d->mbs, d->mbw, d->mbh, d->cqp_off);
     emit_picture(d, d->cur, out, w, h);
-    for (int p = 0; p < 3; p++) { uint8_t *t = d->ref[p]; d->ref[p] = d->cur[p]; d->cur[p] = t; }
-    d->has_ref = 1;
+    if (d->pic_ref) {  /* a reference picture becomes the next P slices' reference; a non-reference one does not */
+        for (int p = 0; p < 3; p++) { uint8_t *t = d->ref[p]; d->ref[p] = d->cur[p]; d->cur[p] = t; }
+        d->has_ref = 1;
+    }
     return 1;
 }
 /* per MB the 24 TotalCoeff bytes (luma raster 0..15, chroma AC 16..23) of the last picture -- test / analysis */

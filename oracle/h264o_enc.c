@@ -749,7 +749,7 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     o += nal_write(tmp + o, 3, idr ? 5 : 1, b.buf, b.len);
     bw_free(&b);
     /* loop filter on the reconstruction -> next reference */
-    deblock_frame(e->rec[0], e->rec[1], e->rec[2], e->cw, e->cw / 2, e->mbs, e->mbw, e->mbh, 0, 0, 0);
+    deblock_frame(e->rec[0], e->rec[1], e->rec[2], e->cw, e->cw / 2, e->mbs, e->mbw, e->mbh, 0);
     for (int p = 0; p < 3; p++) { uint8_t *t = e->ref[p]; e->ref[p] = e->rec[p]; e->rec[p] = t; }
     e->last_qp = qp; e->last_idr = idr;
     e->last_bits = (int64_t)o * 8;

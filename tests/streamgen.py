@@ -122,14 +122,16 @@ class FastBits:
         return np.packbits(bits).tobytes()
 
 
-_I4_NEEDS = {0: 'T', 1: 'L', 2: '', 3: 'T', 4: 'TL', 5: 'TL', 6: 'TL', 7: 'T', 8: 'L'}   # 8.3.1.2.x
-_I16_NEEDS = {0: 'T', 1: 'L', 2: '', 3: 'TL'}                                               # 8.3.3.x
-_CHROMA_NEEDS = {0: '', 1: 'L', 2: 'T', 3: 'TL'}                                            # 8.3.4.x
+# T / L / D: the top / left / top-left neighbour samples (8.3.1.2.x, 8.3.3.x, 8.3.4.x); a slice
+# boundary can leave the top-left macroblock unavailable while the top and left ones are available
+_I4_NEEDS = {0: 'T', 1: 'L', 2: '', 3: 'T', 4: 'TLD', 5: 'TLD', 6: 'TLD', 7: 'T', 8: 'L'}
+_I16_NEEDS = {0: 'T', 1: 'L', 2: '', 3: 'TLD'}
+_CHROMA_NEEDS = {0: '', 1: 'L', 2: 'T', 3: 'TLD'}
 _BLK_ORDER = [0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15]  # decoding order -> raster 4x4
 
 
-def _ok(needs, top, left):
-    return ('T' not in needs or top) and ('L' not in needs or left)
+def _ok(needs, top, left, tl=True):
+    return ('T' not in needs or top) and ('L' not in needs or left) and ('D' not in needs or tl)
 
 
 class SyntaxGen:
@@ -181,17 +183,22 @@ class SyntaxGen:
         return nal(3, 8, w.rbsp())
 
     # ---- helpers
+    def _av(self, mx, my, dx, dy):
+        """macroblock (mx + dx, my + dy) available to (mx, my): in the picture and in the same slice"""
+        x, y = mx + dx, my + dy
+        return 0 <= x < self.mbw and y >= 0 and y * self.mbw + x >= self._first
+
     def _nc(self, nn, avail_mb, mx, my, cur, ras):
         bx, by = ras & 3, ras >> 2
-        na = cur[ras - 1] if bx > 0 else (nn[my][mx - 1][ras + 3] if mx > 0 else None)
-        nb = cur[ras - 4] if by > 0 else (nn[my - 1][mx][ras + 12] if my > 0 else None)
+        na = cur[ras - 1] if bx > 0 else (nn[my][mx - 1][ras + 3] if self._av(mx, my, -1, 0) else None)
+        nb = cur[ras - 4] if by > 0 else (nn[my - 1][mx][ras + 12] if self._av(mx, my, 0, -1) else None)
         return self._avg(na, nb)
 
     def _ncc(self, nn, mx, my, cur, pl, blk):
         base = 16 + 4 * pl
         bx, by = blk & 1, blk >> 1
-        na = cur[base + blk - 1] if bx > 0 else (nn[my][mx - 1][base + blk + 1] if mx > 0 else None)
-        nb = cur[base + blk - 2] if by > 0 else (nn[my - 1][mx][base + blk + 2] if my > 0 else None)
+        na = cur[base + blk - 1] if bx > 0 else (nn[my][mx - 1][base + blk + 1] if self._av(mx, my, -1, 0) else None)
+        nb = cur[base + blk - 2] if by > 0 else (nn[my - 1][mx][base + blk + 2] if self._av(mx, my, 0, -1) else None)
         return self._avg(na, nb)
 
     @staticmethod
@@ -257,7 +264,7 @@ class SyntaxGen:
         """I_NxN / I_16x16 / I_PCM macroblock (mb_type already chosen); returns (qp, nnz row, i4 modes)"""
         rng = self.rng
         cur = [0] * 24
-        top_mb, left_mb = my > 0, mx > 0
+        top_mb, left_mb, tl_mb = self._av(mx, my, 0, -1), self._av(mx, my, -1, 0), self._av(mx, my, -1, -1)
         off = 5 if in_p else 0
         modes = None
         self._last_cbp = 0
@@ -267,7 +274,7 @@ class SyntaxGen:
             for _ in range(384):
                 w.u(int(rng.integers(1, 256)), 8)
             return qp, [16] * 24, None
-        cm = int(rng.choice([m for m, nd in _CHROMA_NEEDS.items() if _ok(nd, top_mb, left_mb)]))
+        cm = int(rng.choice([m for m, nd in _CHROMA_NEEDS.items() if _ok(nd, top_mb, left_mb, tl_mb)]))
         if kind == 'i4':
             w.ue(off + 0)
             modes = [2] * 16
@@ -276,6 +283,8 @@ class SyntaxGen:
                 bx, by = ras & 3, ras >> 2
                 top = by > 0 or top_mb
                 left = bx > 0 or left_mb
+                tl = (bx > 0 and by > 0) or (bx == 0 and by > 0 and left_mb) or (bx > 0 and by == 0 and top_mb) or \
+                     (bx == 0 and by == 0 and tl_mb)
                 # predIntra4x4PredMode (8.3.1.1)
                 if (bx == 0 and not left_mb) or (by == 0 and not top_mb):
                     pm = 2
@@ -283,8 +292,8 @@ class SyntaxGen:
                     a = modes[ras - 1] if bx > 0 else (i4m[my][mx - 1][ras + 3] if kinds[my][mx - 1] == 'i4' else 2)
                     b = modes[ras - 4] if by > 0 else (i4m[my - 1][mx][ras + 12] if kinds[my - 1][mx] == 'i4' else 2)
                     pm = min(a, b)
-                m = int(rng.choice([m for m, nd in _I4_NEEDS.items() if _ok(nd, top, left)]))
-                if rng.random() < 0.3 and _ok(_I4_NEEDS[pm], top, left):
+                m = int(rng.choice([m for m, nd in _I4_NEEDS.items() if _ok(nd, top, left, tl)]))
+                if rng.random() < 0.3 and _ok(_I4_NEEDS[pm], top, left, tl):
                     m = pm
                 modes[ras] = m
                 if m == pm:
@@ -301,7 +310,7 @@ class SyntaxGen:
                 self._residual(w, nn, mx, my, cur, 'i4', cbp, qp, False)
             return qp, cur, modes
         # I_16x16
-        pm16 = int(rng.choice([m for m, nd in _I16_NEEDS.items() if _ok(nd, top_mb, left_mb)]))
+        pm16 = int(rng.choice([m for m, nd in _I16_NEEDS.items() if _ok(nd, top_mb, left_mb, tl_mb)]))
         cbpc = int(rng.integers(0, 3))
         cbpl = 15 if rng.random() < 0.5 else 0
         self._last_cbp = cbpl | (cbpc << 4)
@@ -311,12 +320,11 @@ class SyntaxGen:
         self._residual(w, nn, mx, my, cur, 'i16', cbpl | (cbpc << 4), qp, True)
         return qp, cur, None
 
-    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24, ref_idc=2, cbp_fixed=None):
+    def _header(self, w, first_mb, idr, islice, qp_delta, dbk, override, reorder, ref_idc):
+        """slice_header() (7.3.3) -> SliceQPY"""
         rng = self.rng
-        mbw, mbh = self.mbw, self.mbh
-        w = FastBits()
-        w.ue(0)
-        w.ue(7 if idr else 5)
+        w.ue(first_mb)
+        w.ue(7 if islice else 5)
         w.ue(0)
         w.u(self.frame_num & 0xffff, 16)
         if idr:
@@ -324,8 +332,8 @@ class SyntaxGen:
         if self.poc_type == 0:
             w.u(self.poc & 0xffff, 16)
         elif self.poc_type == 1 and not self.dpoaz:
-            w.se(int(rng.integers(-3, 4)))    # delta_pic_order_cnt[0]
-        if not idr:
+            w.se(self._dpoc)                  # delta_pic_order_cnt[0] (the same in every slice)
+        if not islice:
             w.u(1 if override else 0, 1)
             if override:
                 w.ue(0)                       # num_ref_idx_l0_active_minus1
@@ -338,36 +346,60 @@ class SyntaxGen:
         elif ref_idc:                         # dec_ref_pic_marking() only in reference pictures
             w.u(0, 1)
         qp_delta = min(51 - self.init_qp, max(-self.init_qp, qp_delta))  # SliceQPY in 0..51
-        qp = self.init_qp + qp_delta
         w.se(qp_delta)
         idc, fa, fb = dbk
         w.ue(idc)
         if idc != 1:
             w.se(fa); w.se(fb)
+        return self.init_qp + qp_delta
+
+    def _slice(self, idr, mix, qp_delta=0, dbk=(0, 0, 0), override=False, reorder=False, max_mvd=24, ref_idc=2, cbp_fixed=None,
+               slices=None):
+        """one picture; slices = [{'first': first_mb_in_slice, 'qp_delta', 'dbk', 'intra'}, ...] (first 0 first,
+        increasing; a key left out takes the picture-wide argument) -> the RBSP of each slice in
+        raster order (the single-slice default returns one)"""
+        rng = self.rng
+        mbw, mbh = self.mbw, self.mbh
+        slices = slices or [{'first': 0}]
+        assert slices[0]['first'] == 0 and all(a['first'] < b['first'] for a, b in zip(slices, slices[1:]))
+        self._dpoc = int(rng.integers(-3, 4))
         nn = [[None] * mbw for _ in range(mbh)]
         i4m = [[None] * mbw for _ in range(mbh)]
         kinds = [[None] * mbw for _ in range(mbh)]
         names = list(mix)
         probs = np.array([mix[k] for k in names], float)
         probs /= probs.sum()
-        run = 0
         self.log = []   # per MB: (mb type code as h264o_dec_mbinfo reports it, QPY, coded_block_pattern)
+        out = []
+        w, run, si, islice, qp = None, 0, -1, idr, 0
         for my in range(mbh):
             for mx in range(mbw):
+                addr = my * mbw + mx
+                if si + 1 < len(slices) and addr == slices[si + 1]['first']:
+                    if w is not None:
+                        if run:
+                            w.ue(run)
+                        out.append(w.rbsp())
+                    si += 1
+                    sd = slices[si]
+                    self._first = addr
+                    islice = idr or sd.get('intra', False)
+                    w, run = FastBits(), 0
+                    qp = self._header(w, addr, idr, islice, sd.get('qp_delta', qp_delta), sd.get('dbk', dbk), override, reorder, ref_idc)
                 kind = names[int(rng.choice(len(names), p=probs))]
-                if idr and kind in ('skip', 'p16', 'p16x8', 'p8x16', 'p8x8'):
+                if islice and kind in ('skip', 'p16', 'p16x8', 'p8x16', 'p8x8'):
                     kind = 'i4'
                 if kind == 'skip':
                     run += 1
                     nn[my][mx], kinds[my][mx] = [0] * 24, 'skip'
                     self.log.append((3, qp, 0))
                     continue
-                if not idr:
+                if not islice:
                     w.ue(run)
                     run = 0
                 kinds[my][mx] = kind
                 if kind in ('i4', 'i16', 'pcm'):
-                    qp, nn[my][mx], i4m[my][mx] = self._intra(w, nn, i4m, kinds, mx, my, qp, not idr, kind)
+                    qp, nn[my][mx], i4m[my][mx] = self._intra(w, nn, i4m, kinds, mx, my, qp, not islice, kind)
                     self.log.append(({'i4': 0, 'i16': 1, 'pcm': 7}[kind], qp, self._last_cbp))
                     continue
                 cur = [0] * 24
@@ -378,10 +410,10 @@ class SyntaxGen:
                         w.se(int(rng.integers(-max_mvd, max_mvd + 1))); w.se(int(rng.integers(-max_mvd, max_mvd + 1)))
                 else:
                     subs = [int(rng.integers(0, 4)) for _ in range(4)]
-                    for s in subs:
-                        w.ue(s)
-                    for s in subs:
-                        for _ in range({0: 1, 1: 2, 2: 2, 3: 4}[s]):
+                    for s_ in subs:
+                        w.ue(s_)
+                    for s_ in subs:
+                        for _ in range({0: 1, 1: 2, 2: 2, 3: 4}[s_]):
                             w.se(int(rng.integers(-max_mvd, max_mvd + 1))); w.se(int(rng.integers(-max_mvd, max_mvd + 1)))
                 cbp = int(rng.integers(0, 48)) if rng.random() < 0.85 else 0
                 if cbp_fixed is not None:
@@ -394,24 +426,27 @@ class SyntaxGen:
                 self.log.append(({'p16': 2, 'p16x8': 4, 'p8x16': 5, 'p8x8': 6}[kind], qp, cbp))
         if run:
             w.ue(run)
-        return w.rbsp()
+        out.append(w.rbsp())
+        return out
 
-    def idr(self, mix=None, **kw):
-        """SPS + PPS + IDR picture (I_NxN / I_16x16 / I_PCM)"""
+    def idr(self, mix=None, order=None, **kw):
+        """SPS + PPS + IDR picture (I_NxN / I_16x16 / I_PCM); slices=[...] (see _slice) splits it, order
+        permutes the slices' NAL units (arbitrary slice order)"""
         self.frame_num, self.poc = 0, 0
-        body = self._slice(True, mix or {'i4': 5, 'i16': 4, 'pcm': 1}, **kw)
+        bodies = self._slice(True, mix or {'i4': 5, 'i16': 4, 'pcm': 1}, **kw)
         self.idr_id = (self.idr_id + 1) & 0xffff
         self.frame_num, self.poc = 1, 2
-        return self.sps() + self.pps() + nal(3, 5, body)
+        return self.sps() + self.pps() + b''.join(nal(3, 5, bodies[i]) for i in (order or range(len(bodies))))
 
-    def p(self, mix=None, ref_idc=2, **kw):
-        """one P picture with every macroblock type (ref_idc 0: a non-reference picture)"""
+    def p(self, mix=None, ref_idc=2, order=None, **kw):
+        """one P picture with every macroblock type (ref_idc 0: a non-reference picture); slices=[...]
+        (see _slice) splits it, a slice with 'intra' True is an I slice; order permutes the slices"""
         mix = mix or {'skip': 3, 'p16': 3, 'p16x8': 2, 'p8x16': 2, 'p8x8': 3, 'i4': 1, 'i16': 1, 'pcm': 0.3}
-        body = self._slice(False, mix, ref_idc=ref_idc, **kw)
+        bodies = self._slice(False, mix, ref_idc=ref_idc, **kw)
         if ref_idc:
             self.frame_num = (self.frame_num + 1) & 0xffff
         self.poc += 2
-        return nal(ref_idc, 1, body)
+        return b''.join(nal(ref_idc, 1, bodies[i]) for i in (order or range(len(bodies))))
 
 
 _CHROMA_QP = [i for i in range(30)] + [29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39]

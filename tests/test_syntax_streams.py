@@ -73,11 +73,88 @@ def test_oracle_poc_types(oracle, poc):
         assert [tuple(int(x) for x in r[:3]) for r in mi.reshape(-1, 8)] == log, f'unit {k}'
 
 
-def test_oracle_rejects_non_reference_picture(oracle):
-    """nal_ref_idc 0 (a non-reference P picture, which the wrapper's encoder never emits) is out of the
-    decoder's scope: rejected rather than misparsed (no dec_ref_pic_marking) or used as a reference"""
+def test_oracle_non_reference_picture(oracle):
+    """nal_ref_idc 0 (a non-reference P picture): decoded and output, without dec_ref_pic_marking(), and
+    not used as the next P picture's reference: the P picture after it decodes to the same
+    samples whether or not the non-reference picture was decoded first"""
     from streamgen import SyntaxGen
     g = SyntaxGen(SO, 11, 9, 8)
+    idr, pn, p2 = g.idr(), g.p(ref_idc=0), g.p()
+    a, b = oracle.decoder(), oracle.decoder()
+    assert a.decode(idr)[0] == 1 and b.decode(idr)[0] == 1
+    rc, pic_n, _, _ = a.decode(pn)
+    assert rc == 1
+    ra, pa, _, _ = a.decode(p2)
+    rb, pb, _, _ = b.decode(p2)
+    assert ra == rb == 1 and np.array_equal(pa, pb)
+    assert not np.array_equal(pic_n, pa)
+
+
+# slice layouts (first_mb_in_slice of each slice, per-slice overrides) for an 11 x 9 picture: slices that
+# start mid-row (the top-left / top-right neighbours of their second row lie in the previous slice),
+# several slices in one row, a one-MB slice, I slices inside a P picture, disable_deblocking_filter_idc
+# 0 / 1 / 2 per slice with different offsets and QPs
+MULTI = [
+    [dict(first=0), dict(first=37)],
+    [dict(first=0, dbk=(2, 2, -2)), dict(first=5, qp_delta=3, dbk=(0, -4, 4)), dict(first=16, intra=True, dbk=(2, 0, 0)),
+     dict(first=17), dict(first=60, qp_delta=-6, dbk=(1, 0, 0)), dict(first=98)],
+    [dict(first=k) for k in range(0, 99, 7)],
+]
+
+
+def _multi_units(seed, layout, mbw=11, mbh=9):
+    from streamgen import SyntaxGen
+    g = SyntaxGen(SO, mbw, mbh, seed)
+    units = [(g.idr(slices=layout), g.log)]
+    for _ in range(3):
+        units.append((g.p(slices=layout), g.log))
+    return g, units
+
+
+@pytest.mark.parametrize('layout', range(len(MULTI)))
+def test_oracle_multislice_pictures(oracle, layout):
+    """multi-slice IDR and P pictures (f4): every macroblock parses as generated -- CAVLC contexts, intra
+    mode prediction and P_Skip / motion vector prediction use neighbours of the same slice only -- and
+    the pictures decode (all macroblocks covered exactly once)"""
+    _, units = _multi_units(20 + layout, MULTI[layout])
     d = oracle.decoder()
-    assert d.decode(g.idr())[0] == 1
-    assert d.decode(g.p(ref_idc=0))[0] != 1
+    for k, (u, log) in enumerate(units):
+        rc, _, _, _ = d.decode(u)
+        assert rc == 1, f'unit {k}'
+        mi = np.zeros(11 * 9 * 8, np.int32)
+        oracle.L.h264o_dec_mbinfo(d.d, mi.ctypes.data)
+        assert [tuple(int(x) for x in r[:3]) for r in mi.reshape(-1, 8)] == log, f'unit {k}'
+
+
+def _split_nals(au):
+    starts = [k for k in range(len(au) - 3) if au[k:k + 4] == b'\x00\x00\x00\x01']
+    return [au[a:b] for a, b in zip(starts, starts[1:] + [len(au)])]
+
+
+def test_oracle_arbitrary_slice_order(oracle):
+    """the slices of a picture in any order (ASO, allowed in Baseline) decode to the same picture"""
+    _, units = _multi_units(31, MULTI[1])
+    fwd, rev = oracle.decoder(), oracle.decoder()
+    for k, (u, _) in enumerate(units):
+        nals = _split_nals(u)
+        head = [n for n in nals if n[4] & 31 in (7, 8)]
+        sl = [n for n in nals if n[4] & 31 in (1, 5)]
+        r1, p1, _, _ = fwd.decode(u)
+        r2, p2, _, _ = rev.decode(b''.join(head + sl[::-1]))
+        assert r1 == r2 == 1 and np.array_equal(p1, p2), f'unit {k}'
+
+
+def test_oracle_incomplete_or_overlapping_picture_concealed(oracle):
+    """a picture with a slice missing, or with a slice repeated, is damaged: concealed by the last
+    picture (frame copy, rc 2), which stays the reference"""
+    _, units = _multi_units(32, MULTI[0])
+    d = oracle.decoder()
+    rc, ref_pic, _, _ = d.decode(units[0][0])
+    assert rc == 1
+    sl = _split_nals(units[1][0])
+    rc, pic, _, _ = d.decode(sl[0])                    # second slice missing
+    assert rc == 2 and np.array_equal(pic, ref_pic)
+    rc, pic, _, _ = d.decode(sl[0] + sl[0] + sl[1])    # first slice twice
+    assert rc == 2 and np.array_equal(pic, ref_pic)
+    rc, _, _, _ = d.decode(units[1][0])                # the complete picture still decodes on the IDR
+    assert rc == 1
