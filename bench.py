@@ -70,6 +70,9 @@ def parse():
     ap.add_argument('--recon-cus', type=int, default=0,
                     help='CUs reserved for the reconstruction stream (mask bits [parse_cus, parse_cus + n)); the encoder '
                          'keeps the rest. 0 = reconstruction shares the encoder\'s CUs')
+    ap.add_argument('--streamed', type=int, default=-1, choices=[-1, 0, 1],
+                    help='streamed reconstruction (h264mi_dec_set_streamed); -1: on when the reconstruction stream '
+                         'is kept off the parse CUs (--parse-cus > 0), else the library default')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
@@ -450,6 +453,9 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         dec.set_parse_streams(a.parse_streams)
     if dec is not None and a.parse_cus > 0:
         dec.set_parse_cus(0, a.parse_cus)
+    if dec is not None:
+        dec.set_streamed(a.streamed if a.streamed >= 0 else (1 if a.parse_cus > 0 else -1))
+    streamed_mode = bool(dec.streamed()) if dec is not None else False
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
@@ -590,6 +596,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
+           'streamed_recon': streamed_mode,
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
@@ -628,6 +635,7 @@ def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
         dec.set_parse_streams(a.parse_streams)
     if a.parse_cus > 0:
         dec.set_parse_cus(0, a.parse_cus)
+    dec.set_streamed(a.streamed if a.streamed >= 0 else (1 if a.parse_cus > 0 else -1))
     state = {'t': 0}
 
     def run_steps(k):

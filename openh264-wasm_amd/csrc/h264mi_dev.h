@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include "h264mi_types.h"
 
 #define DEV __device__ __forceinline__

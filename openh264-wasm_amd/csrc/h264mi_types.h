@@ -161,7 +161,13 @@ struct DecFrame {          // per (frame slot, stream): written by dec_scan_kern
     DecParams ps;          // parameter sets in effect for this frame's slices (cropping for the output)
     NalEnt e[H264MI_MAX_NALS];
     SliceEnt sl[H264MI_MAX_SLICES];
+    // streamed reconstruction (runtime_dec.inc): {call tag << 32 | MB rows whose records are
+    // visible to every CU} (H264MI_PROG_ABORT: the slice data failed, no picture), written by the slice-data
+    // waves with agent-scope stores after an L2 write-back; sdone counts the waves done (| failures << 16)
+    uint64_t prog;
+    uint32_t sdone, pad_p;
 };
+#define H264MI_PROG_ABORT 0xFFFFFFFFu
 // MbInfo dword 31 (pad2) of a decoded MB: its slice's first MB (neighbour availability: a preceding MB
 // is in the same slice iff its address >= first) and loop-filter parameters (deblock.inc). 0 for the
 // encoder's single-slice pictures.

@@ -80,6 +80,8 @@ def lib():
             'h264mi_dec_max_frames': (i, [vp]),
             'h264mi_dec_set_parse_streams': (i, [vp, i]),
             'h264mi_dec_set_slice_waves': (i, [vp, i]),
+            'h264mi_dec_set_streamed': (i, [vp, i]),
+            'h264mi_dec_streamed': (i, [vp]),
             'h264mi_dec_set_parse_cus': (i, [vp, i, i]),
             'h264mi_stream_create_cus': (vp, [i, i, i]),
             'h264mi_stream_destroy': (None, [vp]),
@@ -404,6 +406,15 @@ class BatchDecoder:
         """entropy decoding on CU mask bits [lo, hi) (see h264mi_dec_set_parse_cus)"""
         if self._L.h264mi_dec_set_parse_cus(self._d, lo, hi) != 0:
             raise RuntimeError('h264mi_dec_set_parse_cus failed')
+
+    def set_streamed(self, mode):
+        """streamed reconstruction (h264mi_dec_set_streamed): 1 on (the reconstruction stream is kept off the
+        parse CUs), 0 off, -1 automatic"""
+        if self._L.h264mi_dec_set_streamed(self._d, mode) != 0:
+            raise RuntimeError('h264mi_dec_set_streamed failed')
+
+    def streamed(self):
+        return self._L.h264mi_dec_streamed(self._d)
 
     def set_slice_waves(self, k):
         """slice-data waves per picture (h264mi_dec_set_slice_waves): a multi-slice picture's slices in parallel"""

@@ -22,8 +22,15 @@ sys.path.insert(0, os.path.join(ROOT, 'tools'))
     (352, 288, 2000000, 3, 9, 1, 3, 16),    # reserved decode lane: parse on 16 masked CUs, wavefronts on the rest
     (1920, 1080, 1000000, 4, 6, 1, 2, 16),  # the same at the bench geometry
     (1920, 1080, 1000000, 32, 3, 1, 3, 32),  # the bench's own launch: 32 streams, 32 parse CUs, every stream vs its oracle
-], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3', 'cif-lanes16', '1080p-lanes16', '1080p-s32-lanes32'])
+    (176, 144, 300000, 2, 5, 1, 1, 0, 0),      # reconstruction after the parse launch (streamed off)
+    (1920, 1080, 1000000, 4, 6, 1, 2, 16, 0),  # reserved decode lane, streamed off
+    (1920, 1080, 1000000, 2, 5, 1, 1, 0, 1),   # streamed forced without a reserved lane (2 streams: few waves wait)
+], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3', 'cif-lanes16', '1080p-lanes16', '1080p-s32-lanes32',
+        'qcif-unstreamed', '1080p-lanes16-unstreamed', '1080p-streamed-forced'])
 def test_batch_encode_decode(gpu_lib, args):
+    """streamed reconstruction (the first frame of each call row by row behind its slice data) is on in
+    the lanes cases and wherever the library's automatic choice takes it; the *-unstreamed cases pin the
+    launch-after-parse order"""
     import batch_check
     assert batch_check.main(*args)
 

@@ -4,14 +4,16 @@ decode_dev); with G > 1 frames are staged and decoded G at a time (decode_frames
 decode call: decoder status, decoder picture == encoder reconstruction (every stream), and EVERY
 stream's bytes == the bytes of that stream's own oracle encoder (seed s) for every frame. lanes > 0: encoder and reconstruction on streams masked off
 CU bits [0, lanes), entropy decoding (4 parse streams) on those CUs -- the bench's reserved decode lane.
-usage: batch_check.py w h br S nf [dev=1] [G=1] [lanes=0]"""
+streamed: h264mi_dec_set_streamed mode (None: 1 with lanes -- the reconstruction stream is off the parse CUs --,
+else -1, the library's automatic choice).
+usage: batch_check.py w h br S nf [dev=1] [G=1] [lanes=0] [streamed]"""
 import ctypes, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
 
 
-def main(w, h, br, S, nf, dev=1, G=1, lanes=0):
+def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None):
     import torch
     import h264mi
     from h264mi.synth import SyntheticStream
@@ -29,6 +31,8 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0):
     if lanes:
         dec.set_parse_streams(4)
         dec.set_parse_cus(0, lanes)
+    dec.set_streamed((1 if lanes else -1) if streamed is None else streamed)
+    print(f'streamed reconstruction: {dec.streamed()}', flush=True)
     out = np.zeros(w * h * 4, np.uint8)
     slot = 1 << 21
     stage = torch.empty((G, S * slot), dtype=torch.uint8, device='cuda')
