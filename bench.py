@@ -70,6 +70,9 @@ def parse():
     ap.add_argument('--recon-cus', type=int, default=0,
                     help='CUs reserved for the reconstruction stream (mask bits [parse_cus, parse_cus + n)); the encoder '
                          'keeps the rest. 0 = reconstruction shares the encoder\'s CUs')
+    ap.add_argument('--enc-groups', type=int, default=1,
+                    help='the streams are encoded by this many encoders (S / groups streams each) on their own HIP '
+                         'streams, so that one group\'s wavefront ramp overlaps another\'s frame')
     ap.add_argument('--streamed', type=int, default=-1, choices=[-1, 0, 1],
                     help='streamed reconstruction (h264mi_dec_set_streamed); -1: on when the reconstruction stream '
                          'is kept off the parse CUs (--parse-cus > 0), else the library default')
@@ -91,7 +94,7 @@ def parse():
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
-    need = max(8, a.parse_streams + 5)
+    need = max(8, a.parse_streams + 4 + a.enc_groups)
     if int(os.environ.get('GPU_MAX_HW_QUEUES', '4') or 4) < need:
         os.environ['GPU_MAX_HW_QUEUES'] = str(min(need, 32))
     return a
@@ -199,7 +202,8 @@ def measure_traffic(a):
     for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
         d = os.path.join(work, ctr)
         cmd = ['rocprofv3', '--pmc', ctr, '-d', d, '-o', 'run', '--output-format', 'csv', '--', sys.executable,
-               os.path.abspath(__file__), '--traffic-probe', '--config', str(a.config), '--streams', str(a.streams),
+               os.path.abspath(__file__), '--traffic-probe', '--config', str(a.config),
+               '--streams', str(a.streams // max(1, a.enc_groups) if kname == 'enc_mb_kernel' else a.streams),
                '--width', str(a.width), '--height', str(a.height), '--bitrate', str(a.bitrate)]
         try:
             subprocess.run(cmd, cwd='/tmp', env=env, capture_output=True, text=True, timeout=180)
@@ -437,17 +441,22 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # on `ds`, takes G frames per call, entropy-decoding all G x S slices concurrently before
     # reconstructing them in order. NB staging buffers keep NB groups in flight: encoding group g+1
     # overlaps the entropy decoding of g and the reconstruction of g-1.
+    EG = a.enc_groups
+    assert EG >= 1 and S % EG == 0, '--enc-groups must divide the streams'
+    Sg = S // EG
     if a.parse_cus > 0 and a.recon_cus > 0:  # three lanes: entropy decoding, reconstruction, encoder
         hi = a.parse_cus + a.recon_cus
-        es, ds = h264mi.masked_stream(0, hi, True), h264mi.masked_stream(a.parse_cus, hi, False)
+        ess, ds = [h264mi.masked_stream(0, hi, True) for _ in range(EG)], h264mi.masked_stream(a.parse_cus, hi, False)
     elif a.parse_cus > 0:  # wavefront streams off the CUs reserved for entropy decoding
-        es, ds = h264mi.masked_stream(0, a.parse_cus, True), h264mi.masked_stream(0, a.parse_cus, True)
+        ess, ds = [h264mi.masked_stream(0, a.parse_cus, True) for _ in range(EG)], h264mi.masked_stream(0, a.parse_cus, True)
     else:
-        es, ds = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-    enc = h264mi.BatchEncoder(W, H, a.bitrate, S, stream=es)
+        ess, ds = [torch.cuda.Stream(device=dev) for _ in range(EG)], torch.cuda.Stream(device=dev)
+    # EG encoders of Sg streams each, one HIP stream each (stream s = group s // Sg, index s % Sg)
+    encs = [h264mi.BatchEncoder(W, H, a.bitrate, Sg, stream=e) for e in ess]
     # frame skipping off: every step codes a frame (at 1 Mbps the synthetic 1080p content overflows
     # the rate control's buffer and most frames would be dropped)
-    enc.set_frame_skip(False)
+    for enc in encs:
+        enc.set_frame_skip(False)
     dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G) if decode else None
     if dec is not None and a.parse_streams != 3:
         dec.set_parse_streams(a.parse_streams)
@@ -460,7 +469,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
     stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(NB)]
-    ev_enc = [torch.cuda.Event() for _ in range(NB)]
+    ev_enc = [[torch.cuda.Event() for _ in range(EG)] for _ in range(NB)]
     ev_dec = [torch.cuda.Event() for _ in range(NB)]
     gather = NalGather(dist, torch, S, slot, G, rank, world, dev) if world > 1 else None
     # the size all-gather and the sends of a group are ordered after the encoder's staging of that group
@@ -473,21 +482,24 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     def run_group(n):
         b = state['g'] % NB
         t0 = state['t']
-        with torch.cuda.stream(es):
-            es.wait_event(ev_dec[b])  # the decoder has finished with this staging buffer
-            if gather is not None and gather.done_event(b) is not None:
-                es.wait_event(gather.done_event(b))  # and the NAL gather's sends of it
-            for j in range(n):
-                if i_only:
-                    enc.force_idr(-1)
-                enc.encode(clip[(t0 + j) % a.clip])
-                enc.copy_nals(stage[b][j], slot, stage_sz[b][j])
-                if t0 + j < capture:
-                    cap_nal.append((stage[b][j].clone(), stage_sz[b][j].clone()))
-            ev_enc[b].record(es)
+        for k, (enc, es) in enumerate(zip(encs, ess)):
+            with torch.cuda.stream(es):
+                es.wait_event(ev_dec[b])  # the decoder has finished with this staging buffer
+                if gather is not None and gather.done_event(b) is not None:
+                    es.wait_event(gather.done_event(b))  # and the NAL gather's sends of it
+                for j in range(n):
+                    if i_only:
+                        enc.force_idr(-1)
+                    enc.encode(clip[(t0 + j) % a.clip][k * Sg * F:(k + 1) * Sg * F])
+                    enc.copy_nals(stage[b][j][k * Sg * slot:(k + 1) * Sg * slot], slot, stage_sz[b][j][k * Sg:(k + 1) * Sg])
+                ev_enc[b][k].record(es)
         state['t'] = t0 + n
         with torch.cuda.stream(ds):
-            ds.wait_event(ev_enc[b])
+            for e in ev_enc[b]:
+                ds.wait_event(e)
+            for j in range(n):
+                if t0 + j < capture:
+                    cap_nal.append((stage[b][j].clone(), stage_sz[b][j].clone()))
             if decode:
                 base = stage[b].data_ptr()
                 ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
@@ -499,7 +511,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
             ev_dec[b].record(ds)
         if gather is not None:
             with torch.cuda.stream(gs):
-                gs.wait_event(ev_enc[b])
+                for e in ev_enc[b]:
+                    gs.wait_event(e)
                 gather.submit(stage[b], stage_sz[b], n, b)  # sizes gathered once per group; sends of the previous group
         state['g'] += 1
 
@@ -543,14 +556,15 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         n = dec.cw * dec.ch * 3 // 2
         for s in range(S):
             x, y = np.empty(n, np.uint8), np.empty(n, np.uint8)
-            h264mi._hip_memcpy_d2h(x.ctypes.data, enc.recon_ptr(s), n)
+            h264mi._hip_memcpy_d2h(x.ctypes.data, encs[s // Sg].recon_ptr(s % Sg), n)
             h264mi._hip_memcpy_d2h(y.ctypes.data, dec.picture_ptr(s), n)
             selfcheck_ok = selfcheck_ok and bool(np.array_equal(x, y))
-    enc.set_timing(True)
+    for enc in encs:
+        enc.set_timing(True)
     if decode:
         dec.set_timing(True)
     elapsed = timed(run_steps, a.steps, 0, dist, sync)
-    ems, en = enc.kernel_time()
+    ems, en = [sum(x) for x in zip(*[enc.kernel_time() for enc in encs])]
     kern = {'enc_mb_kernel': {'avg_ms': ems / max(en, 1), 'launches': en}}
     gather_check = None
     if gather is not None:  # the last group's units as rank 0 received them == what every rank staged
@@ -578,25 +592,28 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
             prof = np.zeros(nsl * 16, np.uint64)
             h264mi.lib().h264mi_dec_parse_profile(dec._d, prof.ctypes.data)
             kern['dec_parse_kernel']['slice_ms_mean_all_calls'] = float(prof.reshape(-1, 16)[:, 0].sum()) / 1e5 / max(1, (a.warmup + a.steps) * S)
-    sizes = enc.nal_sizes()
-    enc.close()
+    sizes = [x for enc in encs for x in enc.nal_sizes()]
+    for enc in encs:
+        enc.close()
     if dec is not None:
         dec.close()
     if a.parse_cus > 0:
-        h264mi.destroy_stream(es)
+        for es in ess:
+            h264mi.destroy_stream(es)
         h264mi.destroy_stream(ds)
     # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
     # (read source F + read reference F + write reconstruction F) for a P frame, 2F for an IDR
     # 
-    alg = S * (2 if i_only else 3) * F
+    alg = Sg * (2 if i_only else 3) * F  # per launch: one encoder group's streams
     work = {0: 'IPPP encode+decode (intra period 0)', 2: 'I-only encode (force_key_frame before every frame)',
             3: 'IPPP encode+decode (intra period 0), one stream', 5: 'IPPP encode+decode (intra period 0)'}[a.config]
     cfg = {'workload': f'{W}x{H} {work}, {S} streams per GPU, {a.bitrate} bps, wrapper encoder params'
+                       + (f' (encoded by {EG} encoders of {Sg} streams on their own HIP streams)' if EG > 1 else '')
                        + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
-           'streamed_recon': streamed_mode,
+           'streamed_recon': streamed_mode, 'enc_groups': EG,
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
