@@ -73,6 +73,9 @@ def parse():
     ap.add_argument('--enc-groups', type=int, default=1,
                     help='the streams are encoded by this many encoders (S / groups streams each) on their own HIP '
                          'streams, so that one group\'s wavefront ramp overlaps another\'s frame')
+    ap.add_argument('--dec-groups', type=int, default=1,
+                    help='the streams are decoded by this many decoders (S / groups streams each), each reconstructing '
+                         'on its own HIP stream')
     ap.add_argument('--streamed', type=int, default=-1, choices=[-1, 0, 1],
                     help='streamed reconstruction (h264mi_dec_set_streamed); -1: on when the reconstruction stream '
                          'is kept off the parse CUs (--parse-cus > 0), else the library default')
@@ -94,7 +97,7 @@ def parse():
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
-    need = max(8, a.parse_streams + 4 + a.enc_groups)
+    need = max(8, a.dec_groups * (a.parse_streams + 1) + 3 + a.enc_groups)
     if int(os.environ.get('GPU_MAX_HW_QUEUES', '4') or 4) < need:
         os.environ['GPU_MAX_HW_QUEUES'] = str(min(need, 32))
     return a
@@ -441,36 +444,38 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     # on `ds`, takes G frames per call, entropy-decoding all G x S slices concurrently before
     # reconstructing them in order. NB staging buffers keep NB groups in flight: encoding group g+1
     # overlaps the entropy decoding of g and the reconstruction of g-1.
-    EG = a.enc_groups
-    assert EG >= 1 and S % EG == 0, '--enc-groups must divide the streams'
-    Sg = S // EG
+    EG, DG = a.enc_groups, a.dec_groups
+    assert EG >= 1 and S % EG == 0 and DG >= 1 and S % DG == 0, '--enc-groups / --dec-groups must divide the streams'
+    Sg, Sd = S // EG, S // DG
     if a.parse_cus > 0 and a.recon_cus > 0:  # three lanes: entropy decoding, reconstruction, encoder
         hi = a.parse_cus + a.recon_cus
-        ess, ds = [h264mi.masked_stream(0, hi, True) for _ in range(EG)], h264mi.masked_stream(a.parse_cus, hi, False)
+        ess, dss = [h264mi.masked_stream(0, hi, True) for _ in range(EG)], [h264mi.masked_stream(a.parse_cus, hi, False) for _ in range(DG)]
     elif a.parse_cus > 0:  # wavefront streams off the CUs reserved for entropy decoding
-        ess, ds = [h264mi.masked_stream(0, a.parse_cus, True) for _ in range(EG)], h264mi.masked_stream(0, a.parse_cus, True)
+        ess, dss = [h264mi.masked_stream(0, a.parse_cus, True) for _ in range(EG)], [h264mi.masked_stream(0, a.parse_cus, True) for _ in range(DG)]
     else:
-        ess, ds = [torch.cuda.Stream(device=dev) for _ in range(EG)], torch.cuda.Stream(device=dev)
+        ess, dss = [torch.cuda.Stream(device=dev) for _ in range(EG)], [torch.cuda.Stream(device=dev) for _ in range(DG)]
     # EG encoders of Sg streams each, one HIP stream each (stream s = group s // Sg, index s % Sg)
     encs = [h264mi.BatchEncoder(W, H, a.bitrate, Sg, stream=e) for e in ess]
     # frame skipping off: every step codes a frame (at 1 Mbps the synthetic 1080p content overflows
     # the rate control's buffer and most frames would be dropped)
     for enc in encs:
         enc.set_frame_skip(False)
-    dec = h264mi.BatchDecoder(W, H, S, stream=ds, max_frames=G) if decode else None
-    if dec is not None and a.parse_streams != 3:
-        dec.set_parse_streams(a.parse_streams)
-    if dec is not None and a.parse_cus > 0:
-        dec.set_parse_cus(0, a.parse_cus)
-    if dec is not None:
+    # DG decoders of Sd streams each (stream s = decoder s // Sd, index s % Sd), each reconstructing on its
+    # own HIP stream; their entropy decoding shares the reserved parse CUs
+    decs = [h264mi.BatchDecoder(W, H, Sd, stream=d, max_frames=G) for d in dss] if decode else []
+    for dec in decs:
+        if a.parse_streams != 3:
+            dec.set_parse_streams(a.parse_streams)
+        if a.parse_cus > 0:
+            dec.set_parse_cus(0, a.parse_cus)
         dec.set_streamed(a.streamed if a.streamed >= 0 else (1 if a.parse_cus > 0 else -1))
-    streamed_mode = bool(dec.streamed()) if dec is not None else False
+    streamed_mode = all(dec.streamed() for dec in decs) if decs else False
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
     stage = [torch.empty((G, S * slot), dtype=torch.uint8, device=dev) for _ in range(NB)]
     stage_sz = [torch.zeros((G, S), dtype=torch.int32, device=dev) for _ in range(NB)]
     ev_enc = [[torch.cuda.Event() for _ in range(EG)] for _ in range(NB)]
-    ev_dec = [torch.cuda.Event() for _ in range(NB)]
+    ev_dec = [[torch.cuda.Event() for _ in range(DG)] for _ in range(NB)]
     gather = NalGather(dist, torch, S, slot, G, rank, world, dev) if world > 1 else None
     # the size all-gather and the sends of a group are ordered after the encoder's staging of that group
     # only (a stream of their own), never after its decode: NalGather's host reads are one group late
@@ -484,7 +489,8 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         t0 = state['t']
         for k, (enc, es) in enumerate(zip(encs, ess)):
             with torch.cuda.stream(es):
-                es.wait_event(ev_dec[b])  # the decoder has finished with this staging buffer
+                for e in ev_dec[b]:
+                    es.wait_event(e)  # the decoders have finished with this staging buffer
                 if gather is not None and gather.done_event(b) is not None:
                     es.wait_event(gather.done_event(b))  # and the NAL gather's sends of it
                 for j in range(n):
@@ -494,21 +500,24 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                     enc.copy_nals(stage[b][j][k * Sg * slot:(k + 1) * Sg * slot], slot, stage_sz[b][j][k * Sg:(k + 1) * Sg])
                 ev_enc[b][k].record(es)
         state['t'] = t0 + n
-        with torch.cuda.stream(ds):
-            for e in ev_enc[b]:
-                ds.wait_event(e)
-            for j in range(n):
-                if t0 + j < capture:
-                    cap_nal.append((stage[b][j].clone(), stage_sz[b][j].clone()))
-            if decode:
-                base = stage[b].data_ptr()
-                ptrs = [base + j * S * slot + s * slot for j in range(n) for s in range(S)]
-                szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in range(S)]
-                outp = None
-                if t0 < capture:  # every frame's picture of the first frames (parity capture, warmup only)
-                    outp = [cap_pic[t0 + j, s].data_ptr() if t0 + j < capture else 0 for j in range(n) for s in range(S)]
-                dec.decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b], out_ptrs=outp)
-            ev_dec[b].record(ds)
+        for d, ds in enumerate(dss):
+            with torch.cuda.stream(ds):
+                for e in ev_enc[b]:
+                    ds.wait_event(e)
+                if d == 0:
+                    for j in range(n):
+                        if t0 + j < capture:
+                            cap_nal.append((stage[b][j].clone(), stage_sz[b][j].clone()))
+                if decode:
+                    base = stage[b].data_ptr()
+                    ss = range(d * Sd, (d + 1) * Sd)
+                    ptrs = [base + j * S * slot + s * slot for j in range(n) for s in ss]
+                    szp = [stage_sz[b].data_ptr() + 4 * (j * S + s) for j in range(n) for s in ss]
+                    outp = None
+                    if t0 < capture:  # every frame's picture of the first frames (parity capture, warmup only)
+                        outp = [cap_pic[t0 + j, s].data_ptr() if t0 + j < capture else 0 for j in range(n) for s in ss]
+                    decs[d].decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b], out_ptrs=outp)
+                ev_dec[b][d].record(ds)
         if gather is not None:
             with torch.cuda.stream(gs):
                 for e in ev_enc[b]:
@@ -551,17 +560,18 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         cap_pic = None
     selfcheck_ok = True
     if decode:
-        rc, got = dec.status()
-        selfcheck_ok = rc == 0 and all(got)
-        n = dec.cw * dec.ch * 3 // 2
+        for dec in decs:
+            rc, got = dec.status()
+            selfcheck_ok = selfcheck_ok and rc == 0 and all(got)
+        n = decs[0].cw * decs[0].ch * 3 // 2
         for s in range(S):
             x, y = np.empty(n, np.uint8), np.empty(n, np.uint8)
             h264mi._hip_memcpy_d2h(x.ctypes.data, encs[s // Sg].recon_ptr(s % Sg), n)
-            h264mi._hip_memcpy_d2h(y.ctypes.data, dec.picture_ptr(s), n)
+            h264mi._hip_memcpy_d2h(y.ctypes.data, decs[s // Sd].picture_ptr(s % Sd), n)
             selfcheck_ok = selfcheck_ok and bool(np.array_equal(x, y))
     for enc in encs:
         enc.set_timing(True)
-    if decode:
+    for dec in decs:
         dec.set_timing(True)
     elapsed = timed(run_steps, a.steps, 0, dist, sync)
     ems, en = [sum(x) for x in zip(*[enc.kernel_time() for enc in encs])]
@@ -583,24 +593,24 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
             gather_check = got == [h for r in range(world) for h in allh[r]]
         gather_check = {'ok': gather_check, 'units': world * n * S, 'host_waits': gather.host_waits}
     if decode:
-        rms, rn = dec.kernel_time(0)
-        pms, pn = dec.kernel_time(1)
+        rms, rn = [sum(x) for x in zip(*[dec.kernel_time(0) for dec in decs])]
+        pms, pn = [sum(x) for x in zip(*[dec.kernel_time(1) for dec in decs])]
         kern['dec_recon_kernel'] = {'avg_ms': rms / max(rn, 1), 'launches': rn}
-        kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': S * G}
+        kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': Sd * G}
         if os.environ.get('H264MI_PARSE_PROF'):  # diagnostic: the slices' own duration (wave start to end)
-            nsl = S * G * dec.ring_groups()
+            dec = decs[0]
+            nsl = Sd * G * dec.ring_groups()
             prof = np.zeros(nsl * 16, np.uint64)
             h264mi.lib().h264mi_dec_parse_profile(dec._d, prof.ctypes.data)
             kern['dec_parse_kernel']['slice_ms_mean_all_calls'] = float(prof.reshape(-1, 16)[:, 0].sum()) / 1e5 / max(1, (a.warmup + a.steps) * S)
     sizes = [x for enc in encs for x in enc.nal_sizes()]
     for enc in encs:
         enc.close()
-    if dec is not None:
+    for dec in decs:
         dec.close()
     if a.parse_cus > 0:
-        for es in ess:
-            h264mi.destroy_stream(es)
-        h264mi.destroy_stream(ds)
+        for st in ess + dss:
+            h264mi.destroy_stream(st)
     # roofline of the dominant kernel (enc_mb_kernel): algorithmic bytes per launch = S streams x
     # (read source F + read reference F + write reconstruction F) for a P frame, 2F for an IDR
     # 
@@ -613,7 +623,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
-           'streamed_recon': streamed_mode, 'enc_groups': EG,
+           'streamed_recon': streamed_mode, 'enc_groups': EG, 'dec_groups': DG,
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
