@@ -313,6 +313,8 @@ class SyntaxGen:
         pm16 = int(rng.choice([m for m, nd in _I16_NEEDS.items() if _ok(nd, top_mb, left_mb, tl_mb)]))
         cbpc = int(rng.integers(0, 3))
         cbpl = 15 if rng.random() < 0.5 else 0
+        if getattr(self, 'i16_cbp', None) is not None:  # fixed I_16x16 coded_block_pattern (tools/parse_mix.py)
+            cbpc, cbpl = self.i16_cbp >> 4, self.i16_cbp & 15
         self._last_cbp = cbpl | (cbpc << 4)
         w.ue(off + 1 + pm16 + 4 * cbpc + (12 if cbpl else 0))
         w.ue(cm)

@@ -20,6 +20,12 @@ KINDS = [  # name, mix, cbp_fixed, TotalCoeff choices
     ('p16_luma15_tc2', {'p16': 1}, 0x0f, [1, 2, 3]),
     ('p16_all_tc4', {'p16': 1}, 0x2f, [2, 4, 6]),
     ('i16', {'i16': 1}, None, None),
+    # scene-change-like I_16x16 content in P slices (bench frame 22 at 1 Mbps: cbp 47, ~90 % of the luma AC
+    # blocks empty, chroma AC blocks half empty): DC only, luma AC only, chroma only, both
+    ('i16_cbp0', {'i16': 1}, 0x00, [0, 1, 2, 3]),
+    ('i16_luma_sparse', {'i16': 1}, 0x0f, [0] * 9 + [1]),
+    ('i16_chroma_half', {'i16': 1}, 0x20, [0, 0, 1, 1, 2]),
+    ('i16_cbp47_scene', {'i16': 1}, 0x2f, [0] * 9 + [1]),
     ('i4', {'i4': 1}, None, None),
 ]
 
@@ -35,10 +41,11 @@ def main():
     names = ['ring-fill', 'skip-runs', 'mb-hdr', 'residual-rest', 'record', 'qp+ctx', 'luma', 'chromaDC', 'chromaAC']
     only = sys.argv[sys.argv.index('--kind') + 1] if '--kind' in sys.argv else None
     for name, mix, cbp, tcs in KINDS:
-        if only and name != only:
+        if only and name not in only.split(','):
             continue
         g = SyntaxGen(so, 120, 68, 5)
         g.tc_choice = tcs
+        g.i16_cbp = cbp if name.startswith('i16_') else None
         units = [g.idr()] + [g.p(mix, cbp_fixed=cbp) for _ in range(3)]
         dev = [torch.from_numpy(np.frombuffer(u, np.uint8).copy()).cuda() for u in units]
         ms = []
