@@ -77,8 +77,9 @@ def parse():
                     help='the streams are decoded by this many decoders (S / groups streams each), each reconstructing '
                          'on its own HIP stream')
     ap.add_argument('--streamed', type=int, default=-1, choices=[-1, 0, 1],
-                    help='streamed reconstruction (h264mi_dec_set_streamed); -1: on when the reconstruction stream '
-                         'is kept off the parse CUs (--parse-cus > 0), else the library default')
+                    help='streamed reconstruction (h264mi_dec_set_streamed; -1: the library\'s automatic choice, which '
+                         'leaves a 32-stream decoder unstreamed: its 4352 waiting reconstruction waves would hold the CUs '
+                         'the encoder needs while a long slice parses -- profiles/round4/timeline_streamed_tail.txt)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
@@ -471,7 +472,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
             dec.set_parse_streams(a.parse_streams)
         if a.parse_cus > 0:
             dec.set_parse_cus(0, a.parse_cus)
-        dec.set_streamed(a.streamed if a.streamed >= 0 else (1 if a.parse_cus > 0 else -1))
+        dec.set_streamed(a.streamed)
     streamed_mode = all(dec.streamed() for dec in decs) if decs else False
     slot = 1 << 21  # bytes per staged access unit (a 1080p IDR at 1 Mbps is ~100 KB)
     NB = max(2, a.stages)
@@ -665,7 +666,7 @@ def bench_decode_only(a, torch, np, h264mi, SyntheticStream, dev, sync):
         dec.set_parse_streams(a.parse_streams)
     if a.parse_cus > 0:
         dec.set_parse_cus(0, a.parse_cus)
-    dec.set_streamed(a.streamed if a.streamed >= 0 else (1 if a.parse_cus > 0 else -1))
+    dec.set_streamed(a.streamed)
     state = {'t': 0}
 
     def run_steps(k):
