@@ -216,7 +216,7 @@ class SyntaxGen:
         c = np.zeros(maxnum, np.int16)
         if tc:
             pos = rng.choice(maxnum, tc, replace=False)
-            mag = rng.choice([1, 1, 1, 2, 3, 5], tc)
+            mag = rng.choice(getattr(self, 'mag_choice', None) or [1, 1, 1, 2, 3, 5], tc)
             if big_ok and lim > 8 and rng.random() < 0.3:
                 mag[int(rng.integers(tc))] = int(rng.integers(8, lim + 1))   # escape codes (level_prefix 14/15)
             mag = np.minimum(mag, lim)

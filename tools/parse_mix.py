@@ -26,6 +26,12 @@ KINDS = [  # name, mix, cbp_fixed, TotalCoeff choices
     ('i16_luma_sparse', {'i16': 1}, 0x0f, [0] * 9 + [1]),
     ('i16_chroma_half', {'i16': 1}, 0x20, [0, 0, 1, 1, 2]),
     ('i16_cbp47_scene', {'i16': 1}, 0x2f, [0] * 9 + [1]),
+    # chroma AC only (P_L0_16x16, cbp 0x20), every coefficient +-1 (mag1) or 2..3 (mag2): the cost per block kind
+    ('cac_tc1_mag1', {'p16': 1}, 0x20, [1]),
+    ('cac_tc2_mag1', {'p16': 1}, 0x20, [2]),
+    ('cac_tc3_mag1', {'p16': 1}, 0x20, [3]),
+    ('cac_tc1_mag2', {'p16': 1}, 0x20, [1]),
+    ('cac_half_mag1', {'p16': 1}, 0x20, [0, 1, 2]),
     ('i4', {'i4': 1}, None, None),
 ]
 
@@ -46,6 +52,7 @@ def main():
         g = SyntaxGen(so, 120, 68, 5)
         g.tc_choice = tcs
         g.i16_cbp = cbp if name.startswith('i16_') else None
+        g.mag_choice = [1] if name.endswith('_mag1') else ([2, 3] if name.endswith('_mag2') else None)
         units = [g.idr()] + [g.p(mix, cbp_fixed=cbp) for _ in range(3)]
         dev = [torch.from_numpy(np.frombuffer(u, np.uint8).copy()).cuda() for u in units]
         ms = []
