@@ -5,6 +5,8 @@ cycles per macroblock instead).   usage: parse_mix.py [--prof]"""
 import os, sys
 import numpy as np
 PROF = '--prof' in sys.argv
+CNT = bool(os.environ.get('H264MI_LIB', '').endswith('_cnt.so'))  # the -DH264MI_ASM_CNT build
+import ctypes
 if PROF:
     os.environ['H264MI_PARSE_PROF'] = '1'
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -46,6 +48,9 @@ def main():
     NSL = dec.ring_groups()
     names = ['ring-fill', 'skip-runs', 'mb-hdr', 'residual-rest', 'record', 'qp+ctx', 'luma', 'chromaDC', 'chromaAC']
     only = sys.argv[sys.argv.index('--kind') + 1] if '--kind' in sys.argv else None
+    if CNT:
+        L.h264mi_debug_asm_counts.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.h264mi_debug_asm_counts((ctypes.c_uint64 * 16)(), 1)
     for name, mix, cbp, tcs in KINDS:
         if only and name not in only.split(','):
             continue
@@ -71,6 +76,11 @@ def main():
                 if j == len(dev) - 1:
                     print(f'{name:22s} cycles/MB ' + ', '.join(f'{names[k - 3]} {int(d[k]) / nmb:.0f}' for k in range(3, 12)) +
                           f' | total {int(d[3:12].sum()) / nmb:.0f} (slice {int(d[1]) / nmb:.0f})', flush=True)
+        if CNT:  # event counts of the asm MB run per P macroblock (H264MI_ASM_CNT build, tools/README.md)
+            c = (ctypes.c_uint64 * 16)()
+            L.h264mi_debug_asm_counts(c, 1)
+            ev = ['plane', 'pq', 'quiet', 'q-bail', 'blk', 'gen', 'nz1', 'core2', 't23', 'q4', 'mb', 'i16dc', 't1s']
+            print(f'{name:22s} events per MB: ' + ', '.join(f'{ev[k]} {c[k] / (3 * nmb):.2f}' for k in range(13)), flush=True)
         p = float(np.mean(ms[1:]))
         print(f'{name:22s} {np.mean([len(u) for u in units[1:]]):9.0f} B  parse {p:7.3f} ms  {p * 1e6 / nmb:7.1f} ns/MB  '
               f'({p * 2.4e6 / nmb:6.0f} cycles/MB at 2.4 GHz) rc {rc}', flush=True)
