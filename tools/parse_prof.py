@@ -48,6 +48,13 @@ def main(w=1920, h=1080, br=1000000, S=4, nf=8):
         if PMC:
             print(f'frame {t}: {sizes[0]} B rc={rc} decode {dt*1e3:.2f} ms', flush=True)
             continue
+        if os.environ.get('H264MI_LIB', '').endswith('_cnt.so'):  # asm MB-run events per MB (H264MI_ASM_CNT build)
+            c = (ctypes.c_uint64 * 16)()
+            L.h264mi_debug_asm_counts.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            L.h264mi_debug_asm_counts(c, 1)
+            ev = ['plane', 'pq', 'quiet', 'q-bail', 'blk', 'gen', 'nz1', 'core2', 't23', 'q4', 'mb', 'i16dc', 't1s']
+            nmb = S * ((w + 15) // 16) * ((h + 15) // 16)
+            print(f'frame {t}: events per MB ' + ', '.join(f'{ev[k]} {c[k] / nmb:.2f}' for k in range(13)), flush=True)
         cur = np.zeros(NSL * 16, np.uint64)
         L.h264mi_dec_parse_profile(dec._d, cur.ctypes.data)
         d = (cur - prev).reshape(-1, S, 16).sum(0)[0]
