@@ -91,9 +91,9 @@ def parse():
     a.width, a.height = a.width or 1920, a.height or 1080
     a.streams = a.streams or {2: 8, 3: 1, 4: 8, 5: 4}.get(a.config, 32)
     a.group = a.group or (16 if a.config == 4 else 4)
-    # two encoders of 16 streams on their own HIP streams: one's wavefront ramp overlaps the other's frame
-    # (+2-5 % at 32 streams, profiles/round4/ab_enc_groups.txt); one encoder below 16 streams
-    a.enc_groups = a.enc_groups or (2 if a.streams >= 32 and a.streams % 2 == 0 and a.config in (0, 5) else 1)
+    # one encoder: two of 16 streams each on their own HIP streams measured within noise of it (3826-3922 vs
+    # 3738-3902 frames/s over 8 runs, profiles/round4/ab_enc_groups*.txt) and halve the per-launch roofline
+    a.enc_groups = a.enc_groups or 1
     if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
         # a slice wave takes a quarter of a CU's LDS (four per CU): 32 CUs hold the 128 slices of a
         # 32-stream, 4-frame call at once (24 CUs: two rounds); 40 measured slower (profiles/round3/pcus2)
