@@ -138,13 +138,26 @@ def openh264_estimate(a, cores):
                      'scaling over independent streams; an estimate, not a measurement'}
 
 
+def window_args(a, mode):
+    """the CPU leg's window job: frames 0..T (T = the timed pipeline's last frame) of the bench's streams through
+    the oracle, timed over the GPU's own window (warmup..T) and hashed at T. Every stream while T + 1 <= 96
+    frames (32 x 25 1080p frames take ~12 s on 16 host cores); longer runs check as many streams as the host
+    has cores (one stream's serial chain per core) so that the default bench stays within minutes."""
+    if mode == 'dec':
+        return []
+    T = a.warmup + a.steps - 1
+    ns = a.streams if T + 1 <= 96 else min(a.streams, 16)
+    return ['--window-last', str(T), '--window-first', str(a.warmup), '--window-streams', str(ns), '--clip', str(a.clip)]
+
+
 def cpu_baseline(a, mode):
     """the CPU leg (a child process, before this process touches the GPU): the timed baseline, plus the
-    oracle's hashes of the first parity_frames frames of every stream the timed pipeline encodes"""
+    oracle's hashes of the first parity_frames frames of every stream the timed pipeline encodes and of
+    its last timed frame (window_args)"""
     cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
            '--bitrate', str(a.bitrate), '--frames', str(a.cpu_frames), '--mode', mode, '--hash', str(a.parity_frames)]
     if mode != 'dec':
-        cmd += ['--hash-streams', str(a.streams)]
+        cmd += ['--hash-streams', str(a.streams)] + window_args(a, mode)
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])
@@ -241,12 +254,13 @@ def oracle_hashes(a, mode, first):
     child process, no GPU): {str(stream id): [{'nal', 'pic'}, ...]}"""
     cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--width', str(a.width), '--height', str(a.height),
            '--bitrate', str(a.bitrate), '--mode', mode, '--hash', str(a.parity_frames), '--hash-first', str(first),
-           '--hash-streams', str(a.streams), '--hash-only']
+           '--hash-streams', str(a.streams), '--hash-only'] + window_args(a, mode)
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
-        return json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])['parity_hashes_streams']
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith('{')][-1])
+        return d['parity_hashes_streams'], d.get('parity_last')
     except Exception:
-        return {}  # reported as a failed parity check (no hashes)
+        return {}, None  # reported as a failed parity check (no hashes)
 
 
 def gpu_parity(a, oracle_hashes, i_only=False, sid=0):
@@ -298,6 +312,28 @@ def all_stream_parity(captured, shashes, sids, a, decoded):
     return not bad, msg + ('pass' if not bad else f'FAIL (streams {bad[:8]})')
 
 
+def last_frame_parity(got, want, sids, decoded):
+    """the timed pipeline's last frame of every stream the CPU leg ran (all streams unless the run is long;
+    window_args) after the timed region: NAL bytes (and decoded pictures) vs the oracle's sha256"""
+    if not want:
+        return False, 'last timed frame: not checked (no oracle hashes)'
+    if got is None:
+        return False, 'last timed frame: not captured'
+    bad, n, T = [], 0, None
+    for s, sid in enumerate(sids):
+        w = want.get(str(sid))
+        if w is None:
+            continue
+        n += 1
+        T = w['frame']
+        g = got[s]
+        if g['nal'] != w['nal'] or (decoded and g['pic'] != w['pic']):
+            bad.append(sid)
+    what = 'NAL bytes' + (' and decoded pictures' if decoded else '')
+    msg = f'last timed frame {T} of {n} streams ({what}, after the timed region) vs the oracle: '
+    return n > 0 and not bad, msg + ('pass' if n and not bad else f'FAIL (streams {bad[:8]})')
+
+
 def timed(run_steps, K, W, dist, sync):
     run_steps(W)
     sync()
@@ -327,13 +363,14 @@ def main():
     mode = {2: 'enc_i', 4: 'dec'}.get(a.config, 'encdec')
     # CPU baseline + oracle parity hashes first, in child processes, before this process touches the GPU.
     # At N > 1 every rank takes the oracle's hashes of its own first stream (no timing).
-    cpu, hashes, shashes = None, None, None
+    cpu, hashes, shashes, last = None, None, None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, mode)
         hashes = cpu.get('parity_hashes')
         shashes = cpu.get('parity_hashes_streams')
+        last = cpu.get('parity_last')
     elif world > 1 and not a.no_cpu_baseline:
-        shashes = oracle_hashes(a, mode, rank * a.streams)
+        shashes, last = oracle_hashes(a, mode, rank * a.streams)
     a.traffic_kernel = 'dec_recon_kernel' if a.config == 4 else 'enc_mb_kernel'
     a.traffic_measured = (None, 'not measured (--no-traffic or N > 1)')
     if rank == 0 and world == 1 and not a.no_traffic:
@@ -369,6 +406,8 @@ def main():
     elif shashes is not None:
         parity_ok, parity_msg = all_stream_parity(res.pop('captured', None), shashes, stream_ids(rank, a.streams), a,
                                                   decoded=a.config != 2)
+        lok, lmsg = last_frame_parity(res.pop('last_frame', None), last, stream_ids(rank, a.streams), decoded=a.config != 2)
+        parity_ok, parity_msg = parity_ok and lok, parity_msg + '; ' + lmsg
         if world > 1:
             parity_msg = f'rank {rank}: ' + parity_msg
     res.pop('captured', None)
@@ -382,15 +421,24 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity_ok = bool(ok.item())
         if shashes is not None:
-            parity_msg = (f'all {world} ranks x {a.streams} streams x {a.parity_frames} frames of the timed pipeline vs the '
-                          'oracle: ' + ('pass' if parity_ok else 'FAIL'))
+            parity_msg = (f'all {world} ranks x {a.streams} streams x frames 0..{a.parity_frames - 1} and the last timed frame '
+                          f'{a.warmup + a.steps - 1} of the timed pipeline vs the oracle: ' + ('pass' if parity_ok else 'FAIL'))
     frames = res.pop('frames_per_rank') * world
     value = frames / elapsed
     if rank == 0:
         vs = None
         if cpu is not None:
-            cpu = {k: cpu.get(k) for k in ('value', 'unit', 'cores', 'kind', 'sample', 'value_1core', 'build', 'encode_only')
-                   if k in cpu}
+            cpu = {k: cpu.get(k) for k in ('value', 'unit', 'cores', 'kind', 'sample', 'value_1core', 'build', 'encode_only',
+                                           'window') if k in cpu}
+            if cpu.get('window') and cpu['window'].get('value'):
+                # like-for-like: the restatement over the GPU's own timed frames of the same streams is
+                # the line's baseline; the short early-frame sample (frames 1..cpu_frames-1) is kept beside it
+                w_ = cpu.pop('window')
+                cpu['early_frames'] = {k: cpu.pop(k) for k in ('value', 'sample', 'value_1core', 'encode_only') if k in cpu}
+                cpu.update({'value': w_['value'], 'cores': w_['cores'], 'sample': w_['sample'],
+                            'encode_only': {'value': w_['encode_only'], 'unit': 'frames/s', 'cores': w_['cores'],
+                                            'sample': 'encode calls of the same timed frames (decode time excluded)'},
+                            'window_frames': w_['frames'], 'window_streams': w_['streams']})
             est = openh264_estimate(a, cpu.get('cores'))
             if est is not None:
                 cpu['openh264_estimate'] = est
@@ -504,6 +552,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                     enc.copy_nals(stage[b][j][k * Sg * slot:(k + 1) * Sg * slot], slot, stage_sz[b][j][k * Sg:(k + 1) * Sg])
                 ev_enc[b][k].record(es)
         state['t'] = t0 + n
+        state['last'] = (b, n - 1)
         for d, ds in enumerate(dss):
             with torch.cuda.stream(ds):
                 for e in ev_enc[b]:
@@ -567,11 +616,11 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         for dec in decs:
             rc, got = dec.status()
             selfcheck_ok = selfcheck_ok and rc == 0 and all(got)
-        n = decs[0].cw * decs[0].ch * 3 // 2
+        nb = decs[0].cw * decs[0].ch * 3 // 2
         for s in range(S):
-            x, y = np.empty(n, np.uint8), np.empty(n, np.uint8)
-            h264mi._hip_memcpy_d2h(x.ctypes.data, encs[s // Sg].recon_ptr(s % Sg), n)
-            h264mi._hip_memcpy_d2h(y.ctypes.data, decs[s // Sd].picture_ptr(s % Sd), n)
+            x, y = np.empty(nb, np.uint8), np.empty(nb, np.uint8)
+            h264mi._hip_memcpy_d2h(x.ctypes.data, encs[s // Sg].recon_ptr(s % Sg), nb)
+            h264mi._hip_memcpy_d2h(y.ctypes.data, decs[s // Sd].picture_ptr(s % Sd), nb)
             selfcheck_ok = selfcheck_ok and bool(np.array_equal(x, y))
     for enc in encs:
         enc.set_timing(True)
@@ -580,6 +629,25 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     elapsed = timed(run_steps, a.steps, 0, dist, sync)
     ems, en = [sum(x) for x in zip(*[enc.kernel_time() for enc in encs])]
     kern = {'enc_mb_kernel': {'avg_ms': ems / max(en, 1), 'launches': en}}
+    # after the timed region: every stream's last timed frame (NAL units in the last staging slot, the decoders'
+    # current pictures) for the oracle check, and the decoder == reconstruction self-check again
+    sync()
+    lb, lj = state['last']
+    szl = stage_sz[lb][lj].cpu().tolist()
+    hostl = stage[lb][lj].cpu().numpy()
+    last_frame = [{'nal': hashlib.sha256(hostl[s * slot:s * slot + szl[s]].tobytes()).hexdigest(),
+                   'pic': hashlib.sha256(decs[s // Sd].picture_i420(s % Sd)).hexdigest() if decode else None} for s in range(S)]
+    del hostl
+    if decode:
+        for dec in decs:
+            rc, got = dec.status()
+            selfcheck_ok = selfcheck_ok and rc == 0 and all(got)
+        nb = decs[0].cw * decs[0].ch * 3 // 2
+        for s in range(S):
+            x, y = np.empty(nb, np.uint8), np.empty(nb, np.uint8)
+            h264mi._hip_memcpy_d2h(x.ctypes.data, encs[s // Sg].recon_ptr(s % Sg), nb)
+            h264mi._hip_memcpy_d2h(y.ctypes.data, decs[s // Sd].picture_ptr(s % Sd), nb)
+            selfcheck_ok = selfcheck_ok and bool(np.array_equal(x, y))
     gather_check = None
     if gather is not None:  # the last group's units as rank 0 received them == what every rank staged
         sync()
@@ -631,11 +699,12 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False
-    return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg, 'captured': captured,
+    return {'elapsed': elapsed, 'frames_per_rank': S * a.steps, 'config': cfg, 'captured': captured, 'last_frame': last_frame,
             'roofline': roofline('enc_mb_kernel', alg, ems, en, a), 'kernels': kern,
             'nal_gather': gather_check,
             'selfcheck_ok': selfcheck_ok,
-            'selfcheck': ('decoder output == encoder reconstruction for every stream: ' + ('pass' if selfcheck_ok else 'FAIL'))
+            'selfcheck': ('decoder output == encoder reconstruction for every stream, after the warmup and after the timed '
+                          'region: ' + ('pass' if selfcheck_ok else 'FAIL'))
             if decode else 'n/a (encode only)',
             'last_nal_bytes': sizes}
 

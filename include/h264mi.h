@@ -132,10 +132,14 @@ int h264mi_dec_set_slice_waves(h264mi_decoder *d, int k);
    mode 1: on -- the caller guarantees the reconstruction stream never occupies the parse CUs
    (h264mi_dec_set_parse_cus + a stream from h264mi_stream_create_cus(lo, hi, 1)); 0: off; -1 (the
    default): on while the reconstruction waves of all automatically streamed decoders of the process fit
-   in a quarter of the GPU's wave slots (one 1080p stream per decoder does), so that the waiting waves can
+   in h264mi_dec_set_streamed_budget's budget (one 1080p stream per decoder does), so that the waiting waves can
    never keep the parse from a CU. Returns 0, -1 on a bad argument. h264mi_dec_streamed: the mode in effect. */
 int h264mi_dec_set_streamed(h264mi_decoder *d, int mode);
 int h264mi_dec_streamed(h264mi_decoder *d);
+/* automatic streaming's process-wide budget in reconstruction waves (default: a quarter of dec_recon_kernel's
+   resident wave slots on the current device, from its CU count and occupancy); waves <= 0 restores the
+   default. Applies to later h264mi_dec_set_streamed(-1) / decoder creations. Returns the budget in effect. */
+int h264mi_dec_set_streamed_budget(int waves);
 /* entropy decoding on reserved CUs: the parse streams get the CU mask bits [cu_lo, cu_hi) (the runtime
    stripes mask bits over the XCDs); cu_lo == cu_hi removes the mask. Pair with wavefront streams from
    h264mi_stream_create_cus(cu_lo, cu_hi, 1) so that encoder / reconstruction workgroups stay off them. */

@@ -39,7 +39,8 @@ int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax);  /* fi
 void h264o_rc_constants(int32_t out[8]);  /* fps, QP min/max, frame window lower/upper, IDR window, IDR ratio, skip ratio */
 int h264o_table(const char *name, double *out);  /* the oracle's copy of an OpenH264 table (entry count, -1 unknown) */
 int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr);
-size_t h264o_write_sps(int w, int h, uint8_t *out);
+size_t h264o_write_sps(int w, int h, int bitrate, uint8_t *out);
+int h264o_level_idc(int w, int h, int bitrate, int *cs3);
 size_t h264o_write_pps(uint8_t *out);
 
 /* decoder: mirrors init_decoder / decode_frame_yuv_i420 */

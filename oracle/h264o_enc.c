@@ -25,9 +25,12 @@
 #define FRAME_DQP_LOWER 3   /* iFrameDeltaQpLower / iFrameDeltaQpUpper at iRcVaryRatio 0 (func 592) */
 #define FRAME_DQP_UPPER 5
 #define IDR_QP_WINDOW 3     /* RcCalculateIdrQp: the IDR's frame QP window (func 1226) */
-#define LEVEL_FPS 30        /* level_idc choice (this project's rule; not pinned) */
-#define LOG2_MAX_FRAME_NUM 16
-#define LOG2_MAX_POC_LSB 16
+/* Stream syntax OpenH264 writes at the wrapper's parameters, read from the same binary's code
+ * (tools/wasm_syntax.py pins each instruction): WelsInitSps (func 280) stores
+ * uiLog2MaxFrameNum 15 and uiPocType 2 as one i64 constant (file offset 167929), so the slice header
+ * carries a 15-bit frame_num and no POC; the level comes from the level limits at the 60 fps frame
+ * rate and the target bitrate (level_idc_for below). */
+#define LOG2_MAX_FRAME_NUM 15
 #ifndef CROSS_THR
 #define CROSS_THR 1024  /* cross search when the best integer cost exceeds this */
 #endif
@@ -143,47 +146,82 @@ int h264o_table(const char *name, double *out) {
     else if (!strcmp(name, "rc_init_qp")) { for (int i = 0; i < 20; i++) out[n++] = OH_RC_INIT_QP[i / 5][i % 5]; }
     else if (!strcmp(name, "rc_qp_range")) { for (int i = 0; i < 10; i++) out[n++] = OH_RC_QP_RANGE[i / 2][i % 2]; }
     else if (!strcmp(name, "rc_qstep")) { for (int i = 0; i < 52; i++) out[n++] = OH_RC_QSTEP[i]; }
+    else if (!strcmp(name, "level_limits")) { for (int i = 0; i < 17 * 6; i++) out[n++] = OH_LEVEL_LIMITS[i / 6][i % 6]; }
     else return -1;
     return n;
 }
 /* mb_qp_delta carrying QP a from QP_pred b, wrapped into -26..25 (7.4.5) */
 static int qp_delta_wrap(int a, int b) { return ((a - b + 26 + 52) % 52) - 26; }
-static int level_idc_for(int mbs) {
-    static const int L[][3] = {{10, 99, 1485},    {11, 396, 3000},    {12, 396, 6000},     {13, 396, 11880},
-                               {20, 396, 11880},  {21, 792, 19800},   {22, 1620, 20250},   {30, 1620, 40500},
-                               {31, 3600, 108000}, {32, 5120, 216000}, {40, 8192, 245760},  {42, 8704, 522240},
-                               {50, 22080, 589824}, {51, 36864, 983040}, {52, 36864, 2073600}};
-    for (unsigned i = 0; i < sizeof(L) / sizeof(L[0]); i++)
-        if (L[i][1] >= mbs && L[i][2] >= mbs * LEVEL_FPS) return L[i][0];
-    return 52;
+/* level_idc as WelsInitSps chooses it (func 280, file offsets 168119-169382): the first row of the level
+ * limits (OH_LEVEL_LIMITS, in the binary's order) whose MaxMBPS covers the MB rate at the layer's frame
+ * rate (60 fps: the wrapper leaves fMaxFrameRate at its default; (uint32)(60.0f * (float)MBs)), whose MaxFS
+ * covers the frame and 8 * MaxFS covers max(mbw^2, mbh^2), whose MaxDpbMbs covers MBs x num_ref_frames and
+ * whose MaxBR * 1200 covers the target bitrate (the bitrate test is skipped when the bitrate is 0); none:
+ * 51. Level 1b (idc 9) becomes constraint_set3 + idc 11 for Baseline (*cs3 = 1). */
+int h264o_level_idc(int w, int h, int bitrate, int *cs3) {
+    const uint32_t mbw = (uint32_t)(w + 15) >> 4, mbh = (uint32_t)(h + 15) >> 4, mbs = mbw * mbh;
+    const uint32_t sq = mbw * mbw > mbh * mbh ? mbw * mbw : mbh * mbh, dpb = mbs * 1;
+    const uint32_t mbps = (uint32_t)(60.0f * (float)mbs);
+    int level = 51;
+    *cs3 = 0;
+    for (int i = 0; i < 17; i++) {
+        const int32_t *L = OH_LEVEL_LIMITS[i];
+        if ((uint32_t)L[1] < mbps || (uint32_t)L[2] < mbs || ((uint32_t)L[2] << 3) < sq || (uint32_t)L[3] < dpb) continue;
+        if (bitrate && L[4] * 1200 < bitrate) continue;
+        level = L[0];
+        break;
+    }
+    if (level == 9) { *cs3 = 1; level = 11; }
+    return level;
 }
 
 /* ---------------- parameter sets (7.3.2.1 / 7.3.2.2) ---------------- */
-size_t h264o_write_sps(int w, int h, uint8_t *out) {
-    int mbw = (w + 15) / 16, mbh = (h + 15) / 16;
+/* OpenH264's SPS at the wrapper's parameters: WelsInitSps (func 280) fills it, WelsWriteSpsSyntax +
+ * WelsWriteVUI (func 640) write it (DESIGN.md §3.1 lists the file offset of every field):
+ * profile 66; constraint_set0 (Baseline) and constraint_set1 (profile <= 77) set, set2 clear (one layer),
+ * set3 only for level 1b, four reserved zero bits; level_idc (above); sps id 0 (INCREASING_ID never
+ * advances it for a single non-simulcast layer); log2_max_frame_num 15; POC type 2; num_ref_frames 1;
+ * gaps 0; frame_mbs_only 1; direct_8x8_inference = level_idc >= 30; cropping right / bottom by half the
+ * padding; vui_parameters_present 1 with every flag 0 except bitstream_restriction: motion vectors over
+ * picture boundaries 1, max_bytes_per_pic_denom 0, max_bits_per_mb_denom 0, log2_max_mv_length 16 / 16,
+ * max_num_reorder_frames 0, max_dec_frame_buffering = num_ref_frames. */
+size_t h264o_write_sps(int w, int h, int bitrate, uint8_t *out) {
+    int mbw = (w + 15) / 16, mbh = (h + 15) / 16, cs3;
+    const int level = h264o_level_idc(w, h, bitrate, &cs3);
     BW b; bw_init(&b);
     bw_put(&b, 66, 8);            /* profile_idc: Baseline */
-    bw_put(&b, 0xC0, 8);          /* constraint_set0=1, set1=1 */
-    bw_put(&b, level_idc_for(mbw * mbh), 8);
+    bw_put(&b, 0xC0 | (cs3 << 4), 8); /* constraint_set0..3, reserved_zero_4bits */
+    bw_put(&b, level, 8);
     bw_ue(&b, 0);                 /* seq_parameter_set_id */
     bw_ue(&b, LOG2_MAX_FRAME_NUM - 4);
-    bw_ue(&b, 0);                 /* pic_order_cnt_type */
-    bw_ue(&b, LOG2_MAX_POC_LSB - 4);
+    bw_ue(&b, 2);                 /* pic_order_cnt_type */
     bw_ue(&b, 1);                 /* max_num_ref_frames */
     bw_put(&b, 0, 1);             /* gaps_in_frame_num_value_allowed_flag */
     bw_ue(&b, mbw - 1);
     bw_ue(&b, mbh - 1);
     bw_put(&b, 1, 1);             /* frame_mbs_only_flag */
-    bw_put(&b, 1, 1);             /* direct_8x8_inference_flag */
+    bw_put(&b, level >= 30, 1);   /* direct_8x8_inference_flag */
     int crop = (mbw * 16 != w) || (mbh * 16 != h);
     bw_put(&b, crop, 1);
     if (crop) { bw_ue(&b, 0); bw_ue(&b, (mbw * 16 - w) / 2); bw_ue(&b, 0); bw_ue(&b, (mbh * 16 - h) / 2); }
-    bw_put(&b, 0, 1);             /* vui_parameters_present_flag */
+    bw_put(&b, 1, 1);             /* vui_parameters_present_flag */
+    bw_put(&b, 0, 1); bw_put(&b, 0, 1); bw_put(&b, 0, 1); /* aspect_ratio_info, overscan_info, video_signal_type */
+    bw_put(&b, 0, 1); bw_put(&b, 0, 1);                   /* chroma_loc_info, timing_info */
+    bw_put(&b, 0, 1); bw_put(&b, 0, 1); bw_put(&b, 0, 1); /* nal_hrd, vcl_hrd, pic_struct */
+    bw_put(&b, 1, 1);             /* bitstream_restriction_flag */
+    bw_put(&b, 1, 1);             /* motion_vectors_over_pic_boundaries_flag */
+    bw_ue(&b, 0); bw_ue(&b, 0);   /* max_bytes_per_pic_denom, max_bits_per_mb_denom */
+    bw_ue(&b, 16); bw_ue(&b, 16); /* log2_max_mv_length_horizontal / vertical */
+    bw_ue(&b, 0);                 /* max_num_reorder_frames */
+    bw_ue(&b, 1);                 /* max_dec_frame_buffering */
     bw_trailing(&b);
     size_t n = nal_write(out, 3, 7, b.buf, b.len);
     bw_free(&b);
     return n;
 }
+/* OpenH264's PPS (WelsInitPps func 367, WelsWritePpsSyntax func 370): ids 0, CAVLC, one slice group,
+ * num_ref_idx defaults 0, no weighted prediction, pic_init_qp / qs 26, chroma_qp_index_offset 0,
+ * deblocking_filter_control_present 1, constrained_intra_pred 0, redundant_pic_cnt_present 0 */
 size_t h264o_write_pps(uint8_t *out) {
     BW b; bw_init(&b);
     bw_ue(&b, 0); bw_ue(&b, 0);   /* pps id, sps id */
@@ -658,7 +696,7 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
     e->skip_en = 1;  /* the wrapper leaves OpenH264's frame skipping on (bEnableFrameSkip default) */
     e->init_qp = h264o_rc_idr_params(w, h, bitrate, &e->rmin, &e->rmax);
     e->qp = e->init_qp;
-    e->idr_pic_id = -1;
+    e->idr_pic_id = 0;
     return e;
 }
 void h264o_enc_destroy(H264OEnc *e) {
@@ -701,21 +739,33 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     }
     load_source(e, yuv);
     e->first = 0; e->force_idr = 0;
+    /* uiIdrPicId (a uint16) is incremented before the IDR's parameter sets are written (func 589, file
+     * offset 378895), so the first IDR carries 1 when the counter starts at 0 */
     if (idr) { e->frame_num = 0; e->poc = 0; e->idr_pic_id = (e->idr_pic_id + 1) & 0xffff; }
     int qp = rc_frame_qp(e, idr);
     size_t o = 0;
     uint8_t *tmp = (uint8_t *)malloc(64 + (size_t)e->cw * e->ch * 4);
-    if (idr) { o += h264o_write_sps(e->w, e->h, tmp + o); o += h264o_write_pps(tmp + o); }
+    if (idr) { o += h264o_write_sps(e->w, e->h, e->bitrate, tmp + o); o += h264o_write_pps(tmp + o); }
     BW b; bw_init(&b);
-    /* slice_header() 7.3.3 */
+    /* slice_header() 7.3.3 as OpenH264's WelsSliceHeaderWrite (func 1148) writes it with the fields its
+     * slice init (func 225) and WelsUpdateRefSyntax (inlined in func 1017) set:
+     * slice_type 2 (I) / 0 (P), without the +5; no POC field (type 2); a P slice overrides
+     * num_ref_idx_l0_active (1) and reorders its list explicitly: modification_of_pic_nums_idc 0 with
+     * abs_diff_pic_num_minus1 = frame_num - ref frame_num - 1 (0: skipped frames do not advance
+     * frame_num), then 3; IDR marking {no_output_of_prior_pics 0, long_term_reference 0}, P marking
+     * {adaptive_ref_pic_marking_mode 0}; deblocking idc 0 with zero offsets */
     bw_ue(&b, 0);
-    bw_ue(&b, idr ? 7 : 5);
+    bw_ue(&b, idr ? 2 : 0);
     bw_ue(&b, 0);
     bw_put(&b, (uint32_t)e->frame_num, LOG2_MAX_FRAME_NUM);
     if (idr) bw_ue(&b, (uint32_t)e->idr_pic_id);
-    bw_put(&b, (uint32_t)(e->poc & ((1 << LOG2_MAX_POC_LSB) - 1)), LOG2_MAX_POC_LSB);
-    if (!idr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); }
-    if (idr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } else bw_put(&b, 0, 1);
+    if (!idr) {
+        bw_put(&b, 1, 1); bw_ue(&b, 0);                   /* num_ref_idx_active_override_flag, l0 active - 1 */
+        bw_put(&b, 1, 1); bw_ue(&b, 0); bw_ue(&b, 0); bw_ue(&b, 3); /* ref_pic_list_modification_l0 */
+        bw_put(&b, 0, 1);                                  /* adaptive_ref_pic_marking_mode_flag */
+    } else {
+        bw_put(&b, 0, 1); bw_put(&b, 0, 1);                /* no_output_of_prior_pics, long_term_reference */
+    }
     bw_se(&b, qp - 26);
     bw_ue(&b, 0); bw_se(&b, 0); bw_se(&b, 0);
     /* slice_data(): each MB is decided and quantised at its row's QP; an MB that carries

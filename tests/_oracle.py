@@ -22,7 +22,7 @@ class Oracle:
         L.h264o_rc_init_qp.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.h264o_rc_next_qp.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
         L.h264o_write_sps.restype = ctypes.c_size_t
-        L.h264o_write_sps.argtypes = [ctypes.c_int, ctypes.c_int, vp]
+        L.h264o_write_sps.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
         L.h264o_write_pps.restype = ctypes.c_size_t
         L.h264o_write_pps.argtypes = [vp]
         L.h264o_dec_create.restype = vp

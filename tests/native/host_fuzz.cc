@@ -16,7 +16,7 @@
 #include "../../openh264-wasm_amd/csrc/host_sps.h"
 #include "../../openh264-wasm_amd/napi/heap.h"
 
-extern "C" size_t h264o_write_sps(int w, int h, uint8_t *out);  // oracle (linked in by the harness build)
+extern "C" size_t h264o_write_sps(int w, int h, int bitrate, uint8_t *out);  // oracle (linked in by the harness build)
 
 static uint32_t rs = 0x9E3779B9u;
 static uint32_t rnd() { rs ^= rs << 13; rs ^= rs >> 17; rs ^= rs << 5; return rs; }
@@ -27,7 +27,7 @@ static void fuzz_sps() {
     static const int geo[][2] = {{16, 16}, {176, 144}, {1920, 1080}, {98, 62}, {4096, 2160}};
     for (auto &g : geo) {
         uint8_t sps[128];
-        const int n = (int)h264o_write_sps(g[0], g[1], sps);
+        const int n = (int)h264o_write_sps(g[0], g[1], 1000000, sps);
         int w = 0, h = 0;
         CHECK(h264mi::host_peek_sps(sps, n, &w, &h) && w == (g[0] + 15) / 16 && h == (g[1] + 15) / 16,
               "intact SPS %dx%d -> %dx%d MBs", g[0], g[1], w, h);
@@ -49,7 +49,7 @@ static void fuzz_sps() {
     }
     {  // wider than the decoder supports: the peek must refuse it (the C-ABI keeps its working decoder)
         uint8_t sps[128];
-        const int n = (int)h264o_write_sps(16 * (h264mi::H264MI_MAX_MBS + 1), 64, sps);
+        const int n = (int)h264o_write_sps(16 * (h264mi::H264MI_MAX_MBS + 1), 64, 1000000, sps);
         int w = 0, h = 0;
         CHECK(!h264mi::host_peek_sps(sps, n, &w, &h), "SPS of %d MBs per side accepted", h264mi::H264MI_MAX_MBS + 1);
     }

@@ -62,3 +62,26 @@ def test_streamed_reconstruction_vs_oracle_with_damage(gpu_lib, oracle, lanes):
     dec.close()
     if st is not None:
         h264mi.destroy_stream(st)
+
+
+def test_streamed_budget_from_device(gpu_lib):
+    """automatic streaming's wave budget comes from the device (a quarter of dec_recon_kernel's resident wave
+    slots: CUs x its blocks per CU); a decoder whose reconstruction waves exceed the budget falls back to
+    unstreamed reconstruction, one that fits is streamed (the fixed 1024 did not follow the device)"""
+    import torch
+    import h264mi
+    L = h264mi.lib()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    default = L.h264mi_dec_set_streamed_budget(0)
+    assert 0 < default <= cus * 4 * 8 // 4, (default, cus)  # at most a quarter of 8 waves per SIMD
+    try:
+        assert L.h264mi_dec_set_streamed_budget(8) == 8
+        dec = h264mi.BatchDecoder(176, 144, 1)  # 2 x 9 MB rows = 18 waves > 8: unstreamed
+        assert dec.streamed() == 0
+        dec.close()
+        assert L.h264mi_dec_set_streamed_budget(0) == default
+        dec = h264mi.BatchDecoder(176, 144, 1)  # 18 waves fit the device budget: streamed
+        assert dec.streamed() == 1
+        dec.close()
+    finally:
+        L.h264mi_dec_set_streamed_budget(0)

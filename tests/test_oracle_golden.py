@@ -49,11 +49,14 @@ def test_openh264_tables_pinned(oracle, name):
     """The oracle's OpenH264 tables (quantiser MF / FF, lambda, rate-control tables) equal the copies the
     reference's own scripts/h264.wasm holds (tools/wasm_tables.py reads them as bytes)."""
     t = OH['tables'][name]
-    n = int(np.prod(t['shape']))
+    want = np.array(t['values'], dtype=np.float64)
+    if name == 'level_limits':  # the oracle holds the columns WelsInitSps reads (idc .. MaxCPB), not the MV limits
+        want = want[:, :6]
+    n = want.size
     buf = (ctypes.c_double * n)()
     oracle.L.h264o_table.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
     assert oracle.L.h264o_table(name.encode(), buf) == n
-    assert list(buf) == list(np.array(t['values'], dtype=np.float64).reshape(-1)), name
+    assert list(buf) == list(want.reshape(-1)), name
 
 
 def test_openh264_rc_constants_pinned(oracle):
@@ -167,9 +170,138 @@ def test_motion_search_stages_exercised(oracle):
 
 def test_parameter_sets_are_baseline(oracle):
     buf = np.zeros(64, np.uint8)
-    n = oracle.L.h264o_write_sps(1920, 1080, buf.ctypes.data)
+    n = oracle.L.h264o_write_sps(1920, 1080, 1000000, buf.ctypes.data)
     sps = bytes(buf[:n])
     assert sps[:5] == b'\x00\x00\x00\x01\x67'   # 4-byte start code, nal_ref_idc 3, SPS
     assert sps[5] == 66                          # profile_idc Baseline
     n = oracle.L.h264o_write_pps(buf.ctypes.data)
     assert bytes(buf[:5]) == b'\x00\x00\x00\x01\x68'
+
+
+# ---- stream syntax pinned to h264.wasm's code (tools/wasm_tables.py code_constants)
+class Bits:
+    def __init__(self, nal):
+        rbsp, z = bytearray(), 0
+        for c in nal[5:]:  # after the 4-byte start code and the NAL header; emulation prevention removed
+            if z >= 2 and c == 3:
+                z = 0
+                continue
+            rbsp.append(c)
+            z = z + 1 if c == 0 else 0
+        self.b, self.p = bytes(rbsp), 0
+
+    def u(self, n):
+        v = 0
+        for _ in range(n):
+            v = (v << 1) | ((self.b[self.p >> 3] >> (7 - (self.p & 7))) & 1)
+            self.p += 1
+        return v
+
+    def ue(self):
+        z = 0
+        while not self.u(1):
+            z += 1
+        return (1 << z) - 1 + self.u(z)
+
+    def se(self):
+        k = self.ue()
+        return (k + 1) // 2 if k & 1 else -(k // 2)
+
+
+def level_from_fixture(w, h, br):
+    """WelsInitSps's level search (func 280) restated from the fixture alone"""
+    c, rows = OH['code_constants'], OH['tables']['level_limits']['values']
+    mbw, mbh = (w + 15) >> 4, (h + 15) >> 4
+    mbs = mbw * mbh
+    mbps = int(np.float32(np.float32(c['default_max_frame_rate']['value']) * np.float32(mbs)))
+    for idc, maxmbps, maxfs, maxdpb, maxbr, *_ in rows:
+        if maxmbps >= mbps and maxfs >= mbs and 8 * maxfs >= max(mbw * mbw, mbh * mbh) and maxdpb >= mbs and \
+                (br == 0 or maxbr * c['sps_level_maxbr_factor']['value'] >= br):
+            return (11, 1) if idc == 9 else (idc, 0)
+    return c['sps_level_fallback']['value'], 0
+
+
+@pytest.mark.parametrize('w,h', [(176, 144), (208, 120), (352, 288), (640, 360), (1280, 720), (1920, 1080), (3840, 2160),
+                                 (64, 64), (16, 16), (1024, 16)])
+@pytest.mark.parametrize('br', [0, 64000, 300000, 1000000, 8000000, 30000000, 300000000])
+def test_level_idc_pinned(oracle, w, h, br):
+    cs3 = ctypes.c_int()
+    oracle.L.h264o_level_idc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    got = oracle.L.h264o_level_idc(w, h, br, ctypes.byref(cs3))
+    assert (got, cs3.value) == level_from_fixture(w, h, br)
+
+
+def test_sps_pps_syntax_pinned(oracle):
+    """every field of the oracle's SPS / PPS against the h264.wasm facts (WelsInitSps / WelsWriteSpsSyntax /
+    WelsWriteVUI, WelsInitPps / WelsWritePpsSyntax)"""
+    c = {k: v['value'] for k, v in OH['code_constants'].items()}
+    buf = np.zeros(128, np.uint8)
+    for w, h, br in [(1920, 1080, 1000000), (1280, 720, 8000000), (176, 144, 300000), (208, 120, 500000)]:
+        n = oracle.L.h264o_write_sps(w, h, br, buf.ctypes.data)
+        assert bytes(buf[:5]) == b'\x00\x00\x00\x01\x67'
+        r = Bits(bytes(buf[:n]))
+        level, cs3 = level_from_fixture(w, h, br)
+        assert r.u(8) == c['sps_default_profile']
+        assert r.u(8) == 0xC0 | (cs3 << 4)
+        assert r.u(8) == level
+        assert r.ue() == 0
+        assert r.ue() + 4 == c['sps_log2_max_frame_num_and_poc_type'] & 0xffffffff   # 15
+        assert r.ue() == c['sps_log2_max_frame_num_and_poc_type'] >> 32              # POC type 2
+        assert r.ue() == 1 and r.u(1) == 0
+        mbw, mbh = (w + 15) // 16, (h + 15) // 16
+        assert (r.ue() + 1, r.ue() + 1) == (mbw, mbh)
+        assert r.u(1) == 1 and r.u(1) == int(level > c['sps_direct8x8_level_gt'])
+        crop = r.u(1)
+        assert crop == int(mbw * 16 != w or mbh * 16 != h)
+        if crop:
+            assert [r.ue() for _ in range(4)] == [0, (mbw * 16 - w) // 2, 0, (mbh * 16 - h) // 2]
+        assert r.u(1) == 1                                 # vui_parameters_present_flag
+        assert [r.u(1) for _ in range(8)] == [0] * 8       # aspect .. pic_struct
+        assert r.u(1) == 1 and r.u(1) == 1                 # bitstream_restriction, mv over boundaries
+        mv = c['vui_log2_max_mv_length_code'] - 1          # ue code word 17 = value 16
+        assert [r.ue() for _ in range(6)] == [0, 0, mv, mv, 0, 1]
+        assert r.u(1) == 1 and r.p % 8 == 0 or all(r.u(1) == 0 for _ in range(8 - r.p % 8))
+    n = oracle.L.h264o_write_pps(buf.ctypes.data)
+    r = Bits(bytes(buf[:n]))
+    assert [r.ue(), r.ue(), r.u(1), r.u(1), r.ue(), r.ue(), r.ue(), r.u(1), r.u(2)] == [0] * 9
+    qp = c['pps_pic_init_qp_qs']
+    assert [r.se() + 26, r.se() + 26, r.se()] == [qp & 0xff, qp >> 8, 0]
+    assert [r.u(1), r.u(1), r.u(1)] == [1, 0, 0]
+
+
+def test_slice_headers_pinned(oracle):
+    """IDR and P slice headers of an oracle stream: slice_type without +5, 15-bit frame_num, no POC, the
+    P slice's num_ref_idx override and explicit reordering, the marking flags, nal_ref_idc 3"""
+    from h264mi.synth import SyntheticStream
+    c = {k: v['value'] for k, v in OH['code_constants'].items()}
+    w, h = 176, 144
+    g = SyntheticStream(0, w, h)
+    oe = oracle.encoder(w, h, 2000000)
+    oe.set_frame_skip(False)
+    oracle.L.h264o_enc_force_idr.argtypes = [ctypes.c_void_p]
+    idr_ids = []
+    for t in range(5):
+        if t == 3:
+            oracle.L.h264o_enc_force_idr(oe.e)
+        nal = oe.encode(np.ascontiguousarray(g.frame(t)))
+        starts = [k for k in range(len(nal) - 3) if nal[k:k + 4] == b'\x00\x00\x00\x01']
+        sl = nal[starts[-1]:]
+        idr = t in (0, 3)
+        assert len(starts) == (3 if idr else 1)
+        assert sl[4] >> 5 == c['slice_nal_ref_idc']
+        assert sl[4] & 31 == ((c['idr_slice_type_and_nal'] if idr else c['p_slice_type_and_nal']) >> 32)
+        r = Bits(sl)
+        assert r.ue() == 0
+        assert r.ue() == (c['idr_slice_type_and_nal'] if idr else c['p_slice_type_and_nal']) & 0xffffffff
+        assert r.ue() == 0
+        assert r.u(15) == {0: 0, 1: 1, 2: 2, 3: 0, 4: 1}[t]
+        if idr:
+            idr_ids.append(r.ue())
+            assert [r.u(1), r.u(1)] == [0, 0]
+        else:
+            assert r.u(1) == c['p_num_ref_idx_override'] and r.ue() == 0
+            assert [r.u(1), r.ue(), r.ue(), r.ue()] == [1, 0, 0, c['p_reorder_end_idc']]
+            assert r.u(1) == 0
+        r.se()
+        assert [r.ue(), r.se(), r.se()] == [0, 0, 0]
+    assert idr_ids == [1, 2]

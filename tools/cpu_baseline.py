@@ -7,6 +7,9 @@ Modes (what one timed frame is, matching bench.py's configs):
   encdec  1 IDR untimed, then P frames encoded + decoded        (metric, configs 3 and 5)
   enc_i   every frame forced IDR, encoded                         (config 2)
   dec     the stream is encoded untimed, then its P frames decoded (config 4)
+--window-last T: frames 0..T of the bench's streams through the oracle (encoded + decoded), timed over the GPU's
+own window --window-first..T (like-for-like content: the GPU's timed frames include the synthetic scene change
+at frame 22) and hashed at frame T (the timed pipeline's last frame, checked after the timed region).
 Also (--hash K): sha256 of the oracle's NAL bytes and decoded pictures of the first K frames of stream 0
 -- or, with --hash-streams N, of each of streams F..F+N-1 (--hash-first F; one oracle encoder and decoder
 per stream, in parallel worker processes) -- which bench.py compares with the bytes and pictures of the
@@ -83,6 +86,70 @@ def worker(args):
     return timed, counted, hashes, t_enc
 
 
+def worker_window(args):
+    """One stream through frames 0..T (input frame t % clip, IPPP, skipping off; every frame forced IDR in
+    enc_i mode), every frame encoded and -- except in enc_i mode -- decoded by the oracle. Returns the time of
+    the encode and decode calls of frames first..T (the GPU's timed window: like-for-like content) and the
+    sha256 of frame T's NAL bytes and decoded picture (the timed pipeline's last frame, checked after the
+    timed region)."""
+    stream, w, h, bitrate, T, clip, mode, first = args
+    sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
+    import numpy as np
+    from h264mi.synth import SyntheticStream
+    O = ctypes.CDLL(os.path.join(ROOT, 'oracle', 'build', 'libh264_oracle.so'))
+    O.h264o_enc_create.restype = ctypes.c_void_p
+    O.h264o_dec_create.restype = ctypes.c_void_p
+    vp = ctypes.c_void_p
+    S = SyntheticStream(stream, w, h)
+    frames = [np.ascontiguousarray(S.frame(t)) for t in range(min(clip, T + 1))]
+    e = vp(O.h264o_enc_create(w, h, bitrate))
+    O.h264o_enc_set_frame_skip(e, 0)
+    d = vp(O.h264o_dec_create())
+    out = np.zeros(w * h * 4, np.uint8)
+    pic = np.zeros(w * h * 3 // 2, np.uint8)
+    W, H = ctypes.c_int(), ctypes.c_int()
+    t_enc = t_dec = 0.0
+    n = 0
+    for t in range(T + 1):
+        f = frames[t % clip]
+        t0 = time.perf_counter()
+        if mode == 'enc_i':
+            O.h264o_enc_force_idr(e)
+        n = O.h264o_enc_encode(e, f.ctypes.data_as(vp), out.ctypes.data_as(vp), ctypes.c_int(out.size))
+        t1 = time.perf_counter()
+        if mode != 'enc_i':
+            O.h264o_dec_decode(d, out.ctypes.data_as(vp), ctypes.c_int(n), pic.ctypes.data_as(vp), ctypes.byref(W), ctypes.byref(H))
+        t2 = time.perf_counter()
+        if t >= first:
+            t_enc += t1 - t0
+            t_dec += t2 - t1
+    last = {'frame': T, 'nal': hashlib.sha256(out[:n].tobytes()).hexdigest(),
+            'pic': hashlib.sha256(pic.tobytes()).hexdigest() if mode != 'enc_i' else None}
+    O.h264o_enc_destroy(e)
+    O.h264o_dec_destroy(d)
+    return stream, t_enc, t_dec, T + 1 - first, last
+
+
+def window(streams, w, h, bitrate, T, clip, mode, first, procs):
+    """worker_window over the given streams on `procs` processes; each process's busy time is the sum over
+    its streams, the rate is all timed frames / the busiest process (as run())"""
+    jobs = [(sid, w, h, bitrate, T, clip, mode, first) for sid in streams]
+    with mp.get_context('spawn').Pool(max(1, min(procs, len(jobs)))) as pool:
+        res = pool.map(worker_window, jobs, chunksize=1)
+    per = [0.0] * max(1, min(procs, len(jobs)))
+    per_e = list(per)
+    for k, r in enumerate(res):  # the pool's order is not the assignment; this spreads streams evenly
+        per[k % len(per)] += r[1] + r[2]
+        per_e[k % len(per_e)] += r[1]
+    counted = sum(r[3] for r in res)
+    return {'value': counted / max(per) if max(per) > 0 else None, 'encode_only': counted / max(per_e) if max(per_e) > 0 else None,
+            'unit': 'frames/s', 'cores': len(per), 'frames': f'{first}..{T}', 'streams': len(jobs), 'timed_frames': counted,
+            'sample': f'streams {streams[0]}..{streams[-1]} x frames {first}..{T} (the GPU timed window, same synthetic '
+                      f'inputs, input frame t % {clip}) encoded' + ('' if mode == 'enc_i' else ' + decoded') +
+                      f' by the oracle on {len(per)} processes; value = timed frames / busiest process'}, \
+        {str(r[0]): r[4] for r in res}
+
+
 def host_cores():
     """The CPU share this process may use: the affinity mask, capped by OMP_NUM_THREADS when the
     environment sets it (the GPU box sets 16 = its CPU share; nproc there shows the whole host)."""
@@ -122,6 +189,12 @@ def main():
     ap.add_argument('--hash-only', action='store_true', help='only the parity hashes (no timing; N > 1 ranks)')
     ap.add_argument('--hash-streams', type=int, default=0, help='hash the first K frames of N streams (--hash-first ..)')
     ap.add_argument('--hash-first', type=int, default=0, help='first synthetic stream id of --hash-streams')
+    ap.add_argument('--window-last', type=int, default=-1,
+                    help='T: run frames 0..T of --hash-streams streams (from --hash-first), time frames --window-first..T '
+                         '(the GPU timed window) and hash frame T (the timed pipeline\'s last frame)')
+    ap.add_argument('--window-first', type=int, default=0)
+    ap.add_argument('--window-streams', type=int, default=0, help='streams in the window job (0: --hash-streams)')
+    ap.add_argument('--clip', type=int, default=60, help='input frame t is synthetic frame t % clip (bench.py --clip)')
     a = ap.parse_args()
     allc = a.procs or host_cores()
     streams_hashes = None
@@ -129,9 +202,14 @@ def main():
         jobs = [(sid, a.width, a.height, a.bitrate, a.hash, a.mode, a.hash) for sid in range(a.hash_first, a.hash_first + a.hash_streams)]
         with mp.get_context('spawn').Pool(min(allc, len(jobs))) as pool:
             streams_hashes = {str(j[0]): r[2] for j, r in zip(jobs, pool.map(worker, jobs))}
+    win, last = None, None
+    if a.window_last >= 0:
+        ns = a.window_streams or a.hash_streams or 1
+        win, last = window(list(range(a.hash_first, a.hash_first + ns)), a.width, a.height, a.bitrate, a.window_last, a.clip,
+                           a.mode, a.window_first, allc)
     if a.hash_only:
         if streams_hashes is not None:
-            print(json.dumps({'parity_hashes_streams': streams_hashes}))
+            print(json.dumps({'parity_hashes_streams': streams_hashes, 'parity_last': last, 'window': win}))
             return
         _, _, hashes, _ = worker((a.hash_stream, a.width, a.height, a.bitrate, a.hash, a.mode, a.hash))
         print(json.dumps({'parity_hashes': hashes, 'stream': a.hash_stream}))
@@ -143,7 +221,8 @@ def main():
          'build': 'oracle/build/libh264_oracle.so, gcc -O3 -march=x86-64-v3',
          'sample': f'{allc} procs x 1 stream x {a.frames} frames {a.width}x{a.height} at {a.bitrate} bps '
                    f'({what}; {nn} timed frames, slowest process {bn:.2f} s); 1-core: {n1} frames in {b1:.2f} s',
-         'wall_s': round(w1 + wn, 2), 'parity_hashes': hashes, 'parity_hashes_streams': streams_hashes}
+         'wall_s': round(w1 + wn, 2), 'parity_hashes': hashes, 'parity_hashes_streams': streams_hashes,
+         'window': win, 'parity_last': last}
     if a.mode == 'encdec':  # the encode share of the same timed frames (north_star: "host-CPU encode FPS")
         d['encode_only'] = {'value': en, 'value_1core': e1, 'unit': 'frames/s', 'cores': allc,
                             'sample': 'encode calls of the same timed P frames (decode time excluded)'}

@@ -24,6 +24,12 @@ Where each fact was found (wasm function indices count imports; offsets are file
   func  592  RcInitSequenceParameter (iFrameDeltaQpLower/Upper 401384-401409, skip ratio 401267)
   func  597  parameter validation (iMinQp/iMaxQp defaults 408923-409035)
   func 1023  GetDefaultParams (fMaxFrameRate 690465, bFixRCOverShoot 690589, iIdrBitrateRatio 690580)
+  func  280  WelsInitSps: log2_max_frame_num / POC type, default profile, the level search (167923-169382)
+  func  640  WelsWriteSpsSyntax + WelsWriteVUI (direct_8x8 level test 439081, VUI ue(16) 442600)
+  func  367  WelsInitPps (pic_init_qp / qs 202643)
+  func  225  slice init before WelsSliceHeaderWrite (func 1148): num_ref_idx override 120201
+  func 1017  the encode loop: slice type / NAL type per frame type (665206, 665253), nal_ref_idc 669837,
+             WelsUpdateRefSyntax's reordering commands (673611)
   func 1029  WelsHadamardT4Dc: luma DC Hadamard (x + 1) >> 1 with int16 clip (691446-691537)
   funcs 265/345/534/536  quantiser callers: DC quantised with (int16)(FF[0] << 1), MF[0] >> 1; intra
              rows at FF + 6 rows (345 @190274 load16_u off=96, 536 @283180 i32.const 38992)
@@ -148,6 +154,8 @@ TABLES = {
     'rc_init_qp': (43568, 'i', (4, 5), 'RcCalculateIdrQp initial IDR QP [iBppIndex][i]'),
     'rc_qp_range': (43648, 'i', (5, 2), 'RcCalculateIdrQp {max, min} QP of the IDR [i]'),
     'rc_qstep': (43696, 'i', (52,), 'g_kiQpToQstepTable (RcConvertQp2QStep): round(100 * 2^((qp - 4) / 6))'),
+    'level_limits': (63120, 'i', (17, 8), 'g_ksLevelLimits {level_idc, MaxMBPS, MaxFS, MaxDpbMbs, MaxBR, MaxCPB, MinVmv, MaxVmv} '
+                     '(WelsInitSps, func 280, walks it in this order)'),
 }
 
 # name: (file offset of the instruction, opcode, function, meaning)
@@ -169,6 +177,24 @@ CODE_CONSTANTS = {
     'area_90p': (766979, 'i32.const', 1226, 'iBppIndex 0 when w * h < this (<= 28800)'),
     'area_180p': (766991, 'i32.const', 1226, 'iBppIndex 1 when w * h < this'),
     'area_360p': (767005, 'i32.const', 1226, 'iBppIndex 2 when w * h < this, else 3'),
+    # stream syntax (oracle h264o_write_sps / h264o_enc_encode)
+    'sps_log2_max_frame_num_and_poc_type': (167923, 'i64.const', 280, 'WelsInitSps: one i64 store of '
+                                            '{uiLog2MaxFrameNum (low word), uiPocType (high word)}'),
+    'sps_default_profile': (168044, 'i32.const', 280, 'WelsInitSps: uiProfileIdc when the layer leaves it 0 (Baseline)'),
+    'sps_level_table_address': (168196, 'i32.const', 280, 'WelsInitSps: address of g_ksLevelLimits (tables.level_limits)'),
+    'sps_level_maxbr_factor': (168248, 'i32.const', 280, 'WelsInitSps: a level fits when MaxBR * this >= the target bitrate'),
+    'sps_level_fallback': (168271, 'i32.const', 280, 'WelsInitSps: level_idc when no level fits'),
+    'sps_direct8x8_level_gt': (439081, 'i32.const', 640, 'WelsWriteSpsSyntax: direct_8x8_inference_flag = level_idc > this'),
+    'vui_log2_max_mv_length_code': (442600, 'i32.const', 640, 'WelsWriteVUI: the ue(16) code word (17 in 9 bits) of '
+                                    'log2_max_mv_length_horizontal / vertical'),
+    'pps_pic_init_qp_qs': (202643, 'i32.const', 367, 'WelsInitPps: one u16 store of {iPicInitQp, iPicInitQs} (26, 26)'),
+    'p_slice_type_and_nal': (665206, 'i64.const', 1017, 'P frame: one i64 store of {eSliceType (P_SLICE 0), eNalType (1)}'),
+    'idr_slice_type_and_nal': (665253, 'i64.const', 1017, 'IDR frame: {eSliceType (I_SLICE 2), eNalType (5)}: slice_type '
+                               'is written without the +5'),
+    'slice_nal_ref_idc': (669837, 'i32.const', 1017, 'eNalRefIdc of every slice NAL with one temporal layer'),
+    'p_num_ref_idx_override': (120201, 'i32.const', 225, 'P slice: bNumRefIdxActiveOverrideFlag (uiNumRefIdxL0Active = 1)'),
+    'p_reorder_end_idc': (673611, 'i32.const', 1017, 'WelsUpdateRefSyntax: the second reordering command '
+                          '(modification_of_pic_nums_idc 3) after {idc 0, abs_diff_pic_num_minus1}'),
 }
 
 
