@@ -211,6 +211,12 @@ const int *h264mi_ring_size_dev(h264mi_nal_ring *r, long long ticket);  /* devic
 int h264mi_ring_release(h264mi_nal_ring *r, long long ticket, void *hip_stream);
 /* sync: counters, and ref_counts[slots] if non-NULL */
 int h264mi_ring_stats(h264mi_nal_ring *r, int *published, int *dropped_busy, int *dropped_size, int *ref_counts);
+/* Multi-GPU NAL gather (h264mi/shard.py): h264mi_nal_pack concatenates n staged access units (unit u at
+   src + u * slot, sizes[u] bytes; sizes on the device) into dst in unit order, unit u at the sum of the
+   sizes before it, so a rank sends one message per group; h264mi_nal_unpack is the inverse (rank 0 scatters
+   a received packed buffer into slots). One kernel on hip_stream; n <= 8192. Returns 0, -1 on bad arguments. */
+int h264mi_nal_pack(void *dst, const void *src, size_t slot, const int32_t *sizes, int n, void *hip_stream);
+int h264mi_nal_unpack(void *dst, const void *src, size_t slot, const int32_t *sizes, int n, void *hip_stream);
 
 /* edge colour conversions on the GPU, host buffers (openh264_wrapper.cpp:22-40 and :150-195) */
 int h264mi_rgba_to_i420_host(const unsigned char *rgba, int width, int height, unsigned char *out_i420);

@@ -83,6 +83,8 @@ def lib():
             'h264mi_dec_set_streamed': (i, [vp, i]),
             'h264mi_dec_streamed': (i, [vp]),
             'h264mi_dec_set_streamed_budget': (i, [i]),
+            'h264mi_nal_pack': (i, [vp, vp, ctypes.c_size_t, vp, i, vp]),
+            'h264mi_nal_unpack': (i, [vp, vp, ctypes.c_size_t, vp, i, vp]),
             'h264mi_dec_set_parse_cus': (i, [vp, i, i]),
             'h264mi_stream_create_cus': (vp, [i, i, i]),
             'h264mi_stream_destroy': (None, [vp]),

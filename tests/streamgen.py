@@ -6,8 +6,8 @@ outside the LDS window). This writes P pictures whose macroblocks are P_L0_16x16
 and no residual, or P_Skip runs, on top of the SPS/PPS/IDR access unit of a stream from the
 encoder, so that the decoder output can be checked against the oracle decoder (a restatement of the
 normative decoding process, 8.4). Syntax: 7.3.3 slice_header, 7.3.4 slice_data, 7.3.5 mb_pred with
-the encoder's parameter sets (log2_max_frame_num 16, POC type 0 with 16-bit lsb,
-deblocking_filter_control_present, one reference)."""
+the encoder's parameter sets (OpenH264's, DESIGN.md §3.1: log2_max_frame_num 15, POC type 2 -- no POC
+field in the slice header --, deblocking_filter_control_present, one reference)."""
 import numpy as np
 
 
@@ -49,13 +49,13 @@ def nal(ref_idc, typ, rbsp):
 def p_frame(mbw, mbh, frame_num, poc_lsb, rng, max_mvd=96, skip_prob=0.2, qp_delta=0, dbk_idc=0, first_mb=0):
     """One P access unit: each MB P_Skip (runs) with probability skip_prob, else P_L0_16x16 with a
     random mvd in [-max_mvd, max_mvd] quarter samples and coded_block_pattern 0. first_mb > 0 makes
-    it the second slice of a two-slice picture (MBs first_mb..end)."""
+    it the second slice of a two-slice picture (MBs first_mb..end). poc_lsb is unused: the encoder's SPS
+    has POC type 2 (the order follows frame_num)."""
     w = BitWriter()
     w.ue(first_mb)          # first_mb_in_slice
     w.ue(5)                 # slice_type P (all slices of the picture P)
     w.ue(0)                 # pic_parameter_set_id
-    w.u(frame_num & 0xffff, 16)
-    w.u(poc_lsb & 0xffff, 16)
+    w.u(frame_num & 0x7fff, 15)
     w.u(0, 1)               # num_ref_idx_active_override_flag
     w.u(0, 1)               # ref_pic_list_modification_flag_l0
     w.u(0, 1)               # adaptive_ref_pic_marking_mode_flag

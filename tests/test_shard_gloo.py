@@ -115,7 +115,8 @@ def _group_worker(rank, world, port, q):
                         for i in range(S):
                             ok = ok and grp[(r * n + j) * S + i] == everything[r * S + i][t0 + j]
                 t0 += n
-            q.put(bool(ok and t0 == nframes))
+            # one packed message per sending rank and group, not one per access unit
+            q.put(bool(ok and t0 == nframes and gat.messages == 3 * (world - 1)))
     finally:
         dist.destroy_process_group()
 
@@ -126,8 +127,8 @@ def _snapshot(gat, world, S, slot, sz, n):
 
 @pytest.mark.parametrize('world', [2, 4])
 def test_group_gather_real_units(world):
-    """NalGather (bench.py's N > 1 path): per group of frames one size all-gather, the sends of each
-    group posted one group later; rank 0 receives every rank's access units byte for byte."""
+    """NalGather (bench.py's N > 1 path): per group of frames one size all-gather, each rank's group sent as
+    one packed message one group later; rank 0 receives every rank's access units byte for byte."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()

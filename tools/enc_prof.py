@@ -15,8 +15,12 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
     enc = h264mi.BatchEncoder(w, h, br, S)
     enc.set_frame_skip(False)  # every frame coded, as in bench.py
     L = h264mi.lib()
+    fine = bool(os.environ.get('H264MI_ENC_FINE_BUILD'))  # a -DH264MI_ENC_FINE library: slots 11..15 are finer sections
     names = ['row-start-wait', 'wait-above', 'loads+ctx', 'pskip-test', 'int-ME', 'subpel', 'intra-alt', 'p16-resid', 'I4-search',
              'I-resid', 'outputs', 'F:pskip-pred', 'F:ME-first', 'F:satd-half', 'F:sel+satd-q', 'F:p16-pred']
+    if not fine:  # default build: each wave's own busy time inside the pskip-test section (not part of the total)
+        names[11:15] = ['(w0 int-ME busy)', '(w1 pskip busy)', '(w2 pskip busy)', '(w3 pskip busy)']
+    in_total = list(range(16)) if fine else list(range(11)) + [15]
     prev = np.zeros(32, np.uint64)
     enc.set_timing(True)
     kprev = 0.0
@@ -32,7 +36,7 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
         kms, _ = enc.kernel_time()
         print(f'frame {t}: enc_mb {kms - kprev:.3f} ms (with profiling)', flush=True)
         kprev = kms
-        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[0:16].sum():.0f} | ' +
+        print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[in_total].sum():.0f} | ' +
               ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(0, 16) if d[k] > 0), flush=True)
         dn = ['-', 'tile+prefetch', 'top-wait', 'bS+params', 'filter', 'stores+flush']
         print(f'   deblock cycles/MB: total {d[17:22].sum():.0f} | ' + ', '.join(f'{dn[k]} {d[16 + k]:.0f}' for k in range(1, 6)), flush=True)
