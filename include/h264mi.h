@@ -186,6 +186,10 @@ int h264mi_enc_ref_planes(h264mi_encoder *e, int stream, void *host_out);
 int h264mi_dec_recon_profile(h264mi_decoder *d, uint64_t *out);
 /* diagnostics: section cycle counters, 32 totals: 0..15 enc_mb_kernel, 16..31 the encoder's deblock_kernel (env H264MI_ENC_PROF=1) */
 int h264mi_enc_profile(h264mi_encoder *e, uint64_t *out);
+/* diagnostics (env H264MI_ENC_TL=1 at creation): the last frame's enc_mb_kernel timeline, {start, end} per
+   ticket on the GPU's 100 MHz clock (tickets 0 .. S*mbh-1 MB-row encoders, then the deblocking rows);
+   out holds n >= 4 * S * mbh words. -1 when not enabled. */
+int h264mi_enc_timeline(h264mi_encoder *e, uint64_t *out, int n);
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
 void *h264mi_dec_stream(h264mi_decoder *d);

@@ -95,6 +95,7 @@ def lib():
             'h264mi_dec_status': (i, [vp, vp]),
             'h264mi_dec_parse_profile': (i, [vp, vp]),
             'h264mi_enc_profile': (i, [vp, vp]),
+            'h264mi_enc_timeline': (i, [vp, vp, i]),
             'h264mi_dec_picture_ptr': (vp, [vp, i]),
             'h264mi_dec_coded_size': (i, [vp, vp, vp]),
             'h264mi_dec_stream': (vp, [vp]),
