@@ -25,8 +25,11 @@ sys.path.insert(0, os.path.join(ROOT, 'tools'))
     (176, 144, 300000, 2, 5, 1, 1, 0, 0),      # reconstruction after the parse launch (streamed off)
     (1920, 1080, 1000000, 4, 6, 1, 2, 16, 0),  # reserved decode lane, streamed off
     (1920, 1080, 1000000, 2, 5, 1, 1, 0, 1),   # streamed forced without a reserved lane (2 streams: few waves wait)
+    # the bench's timed regime (frames 5..24 incl. the frame-22 scene change): 4 streams x 25 frames, 1080p, 1 Mbps, skipping
+    # off, 4-frame calls on the reserved lane; bytes == oracle and decoded picture == oracle reconstruction, every frame
+    (1920, 1080, 1000000, 4, 25, 1, 4, 16, None, 1),
 ], ids=['qcif-dev', 'qcif-host', 'cif-batch4', 'crop-batch3', '1080p-batch3', 'cif-lanes16', '1080p-lanes16', '1080p-s32-lanes32',
-        'qcif-unstreamed', '1080p-lanes16-unstreamed', '1080p-streamed-forced'])
+        'qcif-unstreamed', '1080p-lanes16-unstreamed', '1080p-streamed-forced', '1080p-s4-25frames-bench-window'])
 def test_batch_encode_decode(gpu_lib, args):
     """streamed reconstruction (the first frame of each call row by row behind its slice data) is on in
     the lanes cases and wherever the library's automatic choice takes it; the *-unstreamed cases pin the

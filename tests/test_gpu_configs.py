@@ -123,11 +123,12 @@ def _oracle_stream(oracle, w, h, br, nf, sid=0):
 
 @pytest.mark.parametrize('br', [1000000, 8000000], ids=['1mbps', '8mbps'])
 def test_config4_every_frame_8_decoders(gpu_lib, oracle, br):
-    """configs[3]: one 1080p IPPP stream decoded by 8 concurrent decoders, 4 frames per call; EVERY
-    frame's picture of every decoder (per-frame outputs of the batched call) == the oracle's picture"""
+    """configs[3] at its stated span: one 1080p IPPP stream of 60 frames decoded by 8 concurrent decoders,
+    4 frames per call; EVERY frame's picture of every decoder (per-frame outputs of the batched call) ==
+    the oracle's picture"""
     import torch
     import h264mi
-    w, h, nf, S, G = 1920, 1080, 12, 8, 4
+    w, h, nf, S, G = 1920, 1080, 60, 8, 4
     units, pics = _oracle_stream(oracle, w, h, br, nf)
     dev = [torch.from_numpy(np.frombuffer(u, np.uint8).copy()).cuda() for u in units]
     F = w * h * 3 // 2

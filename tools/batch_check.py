@@ -5,15 +5,25 @@ decode call: decoder status, decoder picture == encoder reconstruction (every st
 stream's bytes == the bytes of that stream's own oracle encoder (seed s) for every frame. lanes > 0: encoder and reconstruction on streams masked off
 CU bits [0, lanes), entropy decoding (4 parse streams) on those CUs -- the bench's reserved decode lane.
 streamed: h264mi_dec_set_streamed mode (None: 1 with lanes -- the reconstruction stream is off the parse CUs --,
-else -1, the library's automatic choice).
-usage: batch_check.py w h br S nf [dev=1] [G=1] [lanes=0] [streamed]"""
+else -1, the library's automatic choice). pic: also every stream's decoded picture (cropped) == its oracle
+encoder's reconstruction, after every call. The S oracle encoders run in threads (ctypes drops the GIL).
+usage: batch_check.py w h br S nf [dev=1] [G=1] [lanes=0] [streamed] [pic=0]"""
 import ctypes, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
 
 
-def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None):
+def _crop_i420(a, cw, ch, w, h):
+    y = a[:cw * ch].reshape(ch, cw)[:h, :w]
+    u = a[cw * ch:cw * ch * 5 // 4].reshape(ch // 2, cw // 2)[:h // 2, :w // 2]
+    v = a[cw * ch * 5 // 4:cw * ch * 3 // 2].reshape(ch // 2, cw // 2)[:h // 2, :w // 2]
+    return np.concatenate([y.ravel(), u.ravel(), v.ravel()])
+
+
+def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None, pic=0):
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=min(S, 16))
     import torch
     import h264mi
     from h264mi.synth import SyntheticStream
@@ -33,7 +43,7 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None):
         dec.set_parse_cus(0, lanes)
     dec.set_streamed((1 if lanes else -1) if streamed is None else streamed)
     print(f'streamed reconstruction: {dec.streamed()}', flush=True)
-    out = np.zeros(w * h * 4, np.uint8)
+    outs = [np.zeros(w * h * 4, np.uint8) for _ in range(S)]
     slot = 1 << 21
     stage = torch.empty((G, S * slot), dtype=torch.uint8, device='cuda')
     stage_sz = torch.zeros((G, S), dtype=torch.int32, device='cuda')
@@ -48,10 +58,12 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None):
             with torch.cuda.stream(st) if st is not None else torch.cuda.stream(torch.cuda.current_stream()):
                 enc.encode(torch.from_numpy(host).cuda())
             sizes = enc.nal_sizes()
-            for s, oe in enumerate(oes):
-                m = O.h264o_enc_encode(oe, host[s * F:(s + 1) * F].ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p),
-                                       ctypes.c_int(out.size))
-                same[s] = same[s] and enc.nal_bytes(s, sizes[s]) == out[:m].tobytes()
+
+            def oenc(s):
+                return O.h264o_enc_encode(oes[s], host[s * F:(s + 1) * F].ctypes.data_as(ctypes.c_void_p), outs[s].ctypes.data_as(ctypes.c_void_p),
+                                          ctypes.c_int(outs[s].size))
+            for s, m in enumerate(pool.map(oenc, range(S))):
+                same[s] = same[s] and enc.nal_bytes(s, sizes[s]) == outs[s][:m].tobytes()
             if G > 1:
                 enc.copy_nals(stage[j], slot, stage_sz[j])
         if G == 1:
@@ -78,6 +90,10 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None):
             h264mi._hip_memcpy_d2h(a.ctypes.data, enc.recon_ptr(s), a.size)
             h264mi._hip_memcpy_d2h(b.ctypes.data, dec.picture_ptr(s), b.size)
             eq.append(bool(np.array_equal(a, b)))
+            if pic:
+                r = np.empty(w * h * 3 // 2, np.uint8)
+                O.h264o_enc_recon(oes[s], r.ctypes.data_as(ctypes.c_void_p))
+                eq[-1] = eq[-1] and bool(np.array_equal(_crop_i420(b, cw, ch, w, h), r))
             if not eq[-1] and s == 0:
                 d = np.nonzero(a != b)[0]
                 print('   stream0 first diff', d[0], 'count', len(d), 'luma' if d[0] < cw * ch else 'chroma',
@@ -86,6 +102,7 @@ def main(w, h, br, S, nf, dev=1, G=1, lanes=0, streamed=None):
               f'recon==dec {eq}', flush=True)
         ok = ok and all(same) and rc == 0 and all(got) and all(eq)
         t += n
+    pool.shutdown()
     for oe in oes:
         O.h264o_enc_destroy(oe)
     return ok

@@ -38,6 +38,8 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
         kprev = kms
         print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[in_total].sum():.0f} | ' +
               ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(0, 16) if d[k] > 0), flush=True)
+        print('   per wave: outputs busy to the barrier | MB start to the prefetch commit: ' +
+              ', '.join(f'w{k} {d[24 + k]:.0f} | {d[28 + k]:.0f}' for k in range(4)), flush=True)
         dn = ['-', 'tile+prefetch', 'top-wait', 'bS+params', 'filter', 'stores+flush']
         print(f'   deblock cycles/MB: total {d[17:22].sum():.0f} | ' + ', '.join(f'{dn[k]} {d[16 + k]:.0f}' for k in range(1, 6)), flush=True)
 
