@@ -184,7 +184,8 @@ int h264mi_dec_parse_profile(h264mi_decoder *d, uint64_t *out);
 int h264mi_enc_ref_planes(h264mi_encoder *e, int stream, void *host_out);
 /* diagnostics: dec_recon_kernel section cycle counters, 16 totals (env H264MI_RECON_PROF=1) */
 int h264mi_dec_recon_profile(h264mi_decoder *d, uint64_t *out);
-/* diagnostics: section cycle counters, 32 totals: 0..15 enc_mb_kernel, 16..31 the encoder's deblock_kernel (env H264MI_ENC_PROF=1) */
+/* diagnostics: section cycle counters, 64 totals: 0..15 and 32..51 enc_mb_kernel (tools/enc_prof.py names them), 16..21 the
+   encoder's deblocking rows (env H264MI_ENC_PROF=1; H264MI_ENC_PROF_ROW=r counts MB row r only) */
 int h264mi_enc_profile(h264mi_encoder *e, uint64_t *out);
 /* diagnostics (env H264MI_ENC_TL=1 at creation): the last frame's enc_mb_kernel timeline, {start, end} per
    ticket on the GPU's 100 MHz clock (tickets 0 .. S*mbh-1 MB-row encoders, then the deblocking rows);

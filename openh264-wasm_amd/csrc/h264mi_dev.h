@@ -286,7 +286,30 @@ template <class P> DEV void gran_store2(P base, int idx, uint32_t epoch, uint32_
     gran_store(base + idx + 1, epoch, b);
 #endif
 }
+// Wait until the granule at g carries epoch, polling it alone (one 8-byte load, the same address on every
+// lane: one request). gran_wait / DbkSrcGranules use it on the first stale granule of a set instead of
+// re-polling the whole set: a stale poll of a 128-granule record was ~1.3 KB of fabric reads. false on
+// abort/timeout; spins carries the caller's poll count (abort check every 256).
+#ifndef H264MI_GRAN_WAIT1
+#define H264MI_GRAN_WAIT1 1
+#endif
+template <class P> DEV bool gran_wait1(P g, uint32_t epoch, int32_t *abort_word, unsigned &spins) {
+    for (;; spins++) {
+        if ((spins & 255) == 255) {
+            int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ab || spins > (1u << 24)) {
+                if ((threadIdx.x & 63) == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+        const uint64_t y = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(y >> 32) == epoch) return true;
+    }
+}
+
 // lanes [0, n) each poll one granule; returns false on abort/timeout. Payload of lane's granule in *v.
+// A stale set waits on its first stale granule alone, then reloads the set.
 template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, int32_t *abort_word) {
     int lane = threadIdx.x & 63;
     uint32_t val = 0;
@@ -297,7 +320,11 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
             val = (uint32_t)x;
             ok = (uint32_t)(x >> 32) == epoch;
         }
-        if (__all(ok)) break;
+        const uint64_t bad = __ballot(!ok);
+        if (bad == 0) break;
+#if H264MI_GRAN_WAIT1
+        if (!gran_wait1(g + (int)__builtin_ctzll(bad), epoch, abort_word, spins)) return false;
+#else
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (ab || spins > (1u << 24)) {
@@ -306,6 +333,7 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
             }
         }
         __builtin_amdgcn_s_sleep(1);
+#endif
     }
     *v = val;
     return true;

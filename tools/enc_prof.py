@@ -21,15 +21,17 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
     if not fine:  # default build: each wave's own busy time inside the pskip-test section (not part of the total)
         names[11:15] = ['(w0 int-ME busy)', '(w1 pskip busy)', '(w2 pskip busy)', '(w3 pskip busy)']
     in_total = list(range(16)) if fine else list(range(11)) + [15]
-    prev = np.zeros(32, np.uint64)
+    prev = np.zeros(64, np.uint64)
     enc.set_timing(True)
     kprev = 0.0
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * S
+    if os.environ.get('H264MI_ENC_PROF_ROW'):  # one MB row profiled: per MB of that row
+        nmb = ((w + 15) // 16) * S
     for t in range(nf):
         frames = torch.from_numpy(np.concatenate([g.frame(t) for g in gens])).cuda()
         enc.encode(frames)
         sizes = enc.nal_sizes()
-        cur = np.zeros(32, np.uint64)
+        cur = np.zeros(64, np.uint64)
         L.h264mi_enc_profile(enc._e, cur.ctypes.data)
         d = (cur - prev).astype(np.float64) / nmb
         prev = cur
@@ -38,8 +40,11 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
         kprev = kms
         print(f'frame {t}: {sizes[0]} B; cycles/MB: total {d[in_total].sum():.0f} | ' +
               ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(0, 16) if d[k] > 0), flush=True)
-        print('   per wave: outputs busy to the barrier | MB start to the prefetch commit: ' +
-              ', '.join(f'w{k} {d[24 + k]:.0f} | {d[28 + k]:.0f}' for k in range(4)), flush=True)
+        print('   per wave: outputs busy to the barrier | of which up to the prefetch commit: ' +
+              ', '.join(f'w{k} {d[32 + k]:.0f} | {d[36 + k]:.0f}' for k in range(4)), flush=True)
+        # phase beside the integer search, from its start (sums over the MBs that took it, per MB of the frame)
+        print('   search phase, per wave (test or ME start | first mode or diamond | last task): ' +
+              ', '.join(f'w{k} {d[40 + k]:.0f} | {d[44 + k]:.0f} | {d[48 + k]:.0f}' for k in range(4)), flush=True)
         dn = ['-', 'tile+prefetch', 'top-wait', 'bS+params', 'filter', 'stores+flush']
         print(f'   deblock cycles/MB: total {d[17:22].sum():.0f} | ' + ', '.join(f'{dn[k]} {d[16 + k]:.0f}' for k in range(1, 6)), flush=True)
 

@@ -7,5 +7,9 @@ rc=$?; tail -2 gpurun_out/r5${tag}_enc_tests.log
 if [ $rc -ne 0 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
 timeout -k 10 200 python -u tools/enc_prof.py 1920 1080 1000000 32 6 > gpurun_out/r5${tag}_encprof_s32.txt 2>&1 || exit $?
 grep -A2 "^frame 4: [0-9]" gpurun_out/r5${tag}_encprof_s32.txt
+for r in 0 67; do
+  H264MI_ENC_PROF_ROW=$r timeout -k 10 200 python -u tools/enc_prof.py 1920 1080 1000000 32 6 > gpurun_out/r5${tag}_encprof_s32_row$r.txt 2>&1 || exit $?
+done
+CFGS="0:0 4:0 5:0" TAG=${tag} ./tools/sweep_enc_sched.sh || exit $?
 timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r5${tag}_bench.json 2> gpurun_out/r5${tag}_bench.err
 rc=$?; python3 -c "import json; d=json.load(open('gpurun_out/r5${tag}_bench.json')); print(d['value'], d['ms_per_step'], d['kernels']['enc_mb_kernel'], d['parity']['vs_oracle'][-60:])"; exit $rc
