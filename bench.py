@@ -59,6 +59,10 @@ def parse():
     ap.add_argument('--group', type=int, default=0,
                     help='frames per stream per decode call (frame-parallel entropy decoding); default 4, 16 for the '
                          'decode-only config (no encoder latency to hide: more slices in flight)')
+    ap.add_argument('--tail-streamed', type=int, default=1, choices=[0, 1],
+                    help='reconstruct the frame-by-frame tail calls streamed (h264mi_dec_set_streamed 1: each frame\'s '
+                         'reconstruction rows follow its slice data instead of waiting for the whole parse launch); '
+                         'only with the reserved decode lane, whose CUs the waiting waves cannot take')
     ap.add_argument('--no-tail-frames', dest='tail_frames', action='store_false',
                     help='decode the last group of a run as one call too (default: frame by frame)')
     ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
@@ -578,15 +582,26 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                 gather.submit(stage[b], stage_sz[b], n, b)  # sizes gathered once per group; sends of the previous group
         state['g'] += 1
 
+    tail_streamed = bool(a.tail_streamed and decs and a.parse_cus > 0 and a.tail_frames)
+
+    def set_tail(on):  # the tail's reconstruction streamed behind its slice data (a forced, gated launch)
+        if tail_streamed:
+            for dec in decs:
+                dec.set_streamed(1 if on else a.streamed)
+
     def run_steps(k):
         # groups of G frames; the last group of a run is decoded frame by frame, so the pipeline drains
         # at frame granularity (each of its frames is entropy-decoded as soon as it is encoded, instead of
-        # after the whole group)
+        # after the whole group), and those calls reconstruct streamed: the drain is the tail's slowest slice
+        # (the frame-22 scene change, ~35 ms of one wave's CAVLC chain) plus the reconstructions queued
+        # behind it, and a streamed reconstruction finishes with its parse instead of ~3 ms after it
         while k > 0:
             n = min(G, k)
             if k <= G and a.tail_frames:
+                set_tail(True)
                 for _ in range(n):
                     run_group(1)
+                set_tail(False)
             else:
                 run_group(n)
             k -= n
@@ -695,7 +710,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
-           'streamed_recon': streamed_mode, 'enc_groups': EG, 'dec_groups': DG,
+           'streamed_recon': streamed_mode, 'tail_streamed': tail_streamed, 'enc_groups': EG, 'dec_groups': DG,
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False

@@ -133,7 +133,9 @@ int h264mi_dec_set_slice_waves(h264mi_decoder *d, int k);
    (h264mi_dec_set_parse_cus + a stream from h264mi_stream_create_cus(lo, hi, 1)); 0: off; -1 (the
    default): on while the reconstruction waves of all automatically streamed decoders of the process fit
    in h264mi_dec_set_streamed_budget's budget (one 1080p stream per decoder does), so that the waiting waves can
-   never keep the parse from a CU. Returns 0, -1 on a bad argument. h264mi_dec_streamed: the mode in effect. */
+   never keep the parse from a CU. Applies to the calls enqueued after it (each call captures its mode); it
+   synchronises the decoder's streams only when the decoder gives up an automatic share of the budget.
+   Returns 0, -1 on a bad argument. h264mi_dec_streamed: the mode in effect. */
 int h264mi_dec_set_streamed(h264mi_decoder *d, int mode);
 int h264mi_dec_streamed(h264mi_decoder *d);
 /* automatic streaming's process-wide budget in reconstruction waves (default: a quarter of dec_recon_kernel's
