@@ -2,13 +2,14 @@
 """bench.py -- BASELINE.json metric "1080p30 frames/sec encode+decode per GPU" on MI355X.
 
 Parity: the GPU's NAL bytes and decoded pictures are checked against the oracle (oracle/, the CPU
-restatement of the reference path) on the bench's own geometry and bitrate before timing; parity
-with OpenH264 itself is unpinned. A failed check prints value null and exits 1.
+restatement of the reference path) on the bench's own geometry and bitrate: the first frames of every
+stream (captured in the warmup) and the last timed frame of every stream (captured after the timed
+region); parity with OpenH264 itself is partial. A failed check prints value null and exits 1.
 
 Default workload (the metric; at N > 1 also BASELINE.json configs[4]'s NAL gather): every rank owns
 S streams (default 32: the GPU's 1080p30 throughput comes from concurrent independent streams, SURVEY.md
-§7; at 32 streams a frame step of all of them takes ~13-15 ms, inside the 33 ms of a 30 fps frame
-interval, so every stream runs in real time -- the 8-stream line is kept in profiles/ beside it). One
+§7; at 32 streams a frame step of all of them takes ~7.7 ms, inside the 33 ms of a 30 fps frame
+interval, so every stream runs in real time; 64-128 streams add 10-20 %, DESIGN.md §5 Capacity). One
 step = one frame of each of them: GPU encode (libh264mi batch encoder,
 IPPP, intra period 0, the wrapper's parameters, 1 Mbps) and GPU decode of exactly the NAL units
 produced, plus (N > 1) the gather of those NAL units to rank 0 over RCCL. Frames are encoded on one

@@ -5,7 +5,7 @@ import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 flt = sys.argv[3:] or ['enc_mb_kernel', 'dec_parse_kernel', 'dec_recon_kernel', 'dec_hdr', 'dec_scan', 'enc_copy']
-ks = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0].replace('h264mi::', ''), r.get('Stream_Id', r.get('Queue_Id', '?')), r.get('Queue_Id', '?')) for r in rows)
+ks = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0].split('<')[0].replace('void ', '').replace('h264mi::', ''), r.get('Stream_Id', r.get('Queue_Id', '?')), r.get('Queue_Id', '?')) for r in rows)
 mb = [k for k in ks if k[2] == 'enc_mb_kernel']
 t0 = mb[-steps][0]
 tend = max(k[1] for k in ks)
