@@ -42,6 +42,7 @@ def main(w=1920, h=1080, br=1000000, S=8, nf=6):
               ', '.join(f'{names[k]} {d[k]:.0f}' for k in range(0, 16) if d[k] > 0), flush=True)
         print('   per wave: outputs busy to the barrier | of which up to the prefetch commit: ' +
               ', '.join(f'w{k} {d[32 + k]:.0f} | {d[36 + k]:.0f}' for k in range(4)), flush=True)
+        print('   outputs, per wave (to the end of its first store group): ' + ', '.join(f'w{k} {d[52 + k]:.0f}' for k in range(4)), flush=True)
         # phase beside the integer search, from its start (sums over the MBs that took it, per MB of the frame)
         print('   search phase, per wave (test or ME start | first mode or diamond | last task): ' +
               ', '.join(f'w{k} {d[40 + k]:.0f} | {d[44 + k]:.0f} | {d[48 + k]:.0f}' for k in range(4)), flush=True)
