@@ -1,6 +1,9 @@
 """enc_mb_kernel per-ticket timeline (H264MI_ENC_TL=1): S streams 1080p IPPP at the bench's bitrate, frames 0..nf-1;
 for each frame: the launch span, the encoder rows' and deblocking rows' start / end distribution, and how many
 tickets were live over time (which bounds the kernel: residency, the wavefront ramp, or the deblocking tail).
+With the per-XCD ticket queues (the default when S % 8 == 0; H264MI_ENC_XQ=0 turns them off) the kernel records
+ticket t of XCD queue q at slot q * 2 (S / 8) mbh + t; the slots are put back in the one-queue order (encoder row r
+of stream s at r S + s, its deblocking row at S mbh + r S + s) before anything is summarised.
 usage: enc_timeline.py [w h br S nf]"""
 import os, sys
 os.environ['H264MI_ENC_TL'] = '1'
@@ -25,6 +28,15 @@ def main(w=1920, h=1080, br=1000000, S=32, nf=6):
         tl = np.zeros(n, np.uint64)
         assert L.h264mi_enc_timeline(enc._e, tl.ctypes.data, n) == 0
         tl = tl.reshape(-1, 2).astype(np.int64)
+        if S % 8 == 0 and os.environ.get('H264MI_ENC_XQ', '1') != '0' and int(os.environ.get('H264MI_DBK_LAG', '0')) <= 0:
+            Sq, per = S // 8, 2 * (S // 8) * mbh
+            slot = np.arange(2 * S * mbh)
+            q, tq = slot // per, slot % per
+            tb, s = tq // Sq, (tq % Sq) * 8 + q
+            canon = np.where(tb < mbh, tb * S + s, S * mbh + (tb - mbh) * S + s)
+            out = np.empty_like(tl)
+            out[canon] = tl[:2 * S * mbh]
+            tl = out
         t0 = tl[:, 0].min()
         st, en = (tl[:, 0] - t0) / 100.0, (tl[:, 1] - t0) / 100.0  # microseconds (100 MHz)
         E, D = slice(0, S * mbh), slice(S * mbh, 2 * S * mbh)
