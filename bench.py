@@ -64,6 +64,14 @@ def parse():
                     help='reconstruct the frame-by-frame tail calls streamed (h264mi_dec_set_streamed 1: each frame\'s '
                          'reconstruction rows follow its slice data instead of waiting for the whole parse launch); '
                          'only with the reserved decode lane, whose CUs the waiting waves cannot take')
+    ap.add_argument('--no-decode', action='store_true',
+                    help='diagnostics: encode only (the metric line then counts encoded frames; not the metric)')
+    ap.add_argument('--recon-gate-frac', type=float, default=1.0,
+                    help='with --recon-gate: the fraction of the encoder launch\'s MB rows that must have started')
+    ap.add_argument('--recon-gate', type=int, default=0, choices=[0, 1],
+                    help='start each decoded frame\'s reconstruction once the encoder launch running two frames later has '
+                         'started all its MB rows (h264mi_dec_set_recon_gate on h264mi_enc_rows_counter): the reconstruction '
+                         'then fills the encoder launch\'s tail instead of sharing its densest part')
     ap.add_argument('--no-tail-frames', dest='tail_frames', action='store_false',
                     help='decode the last group of a run as one call too (default: frame by frame)')
     ap.add_argument('--stages', type=int, default=4, help='NAL staging buffers (groups in flight between encoder and decoder)')
@@ -490,7 +498,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     W, H, S, G = a.width, a.height, a.streams, a.group
     F = W * H * 3 // 2
     i_only = a.config == 2
-    decode = not i_only
+    decode = not i_only and not a.no_decode
     clip = torch.empty((a.clip, S * F), dtype=torch.uint8, device=dev)
     for i, sid in enumerate(stream_ids(rank, S)):
         g = SyntheticStream(sid, W, H)
@@ -541,7 +549,9 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
     cap_nal = []  # (stage copy, sizes copy) of frames 0..capture-1
     cap_pic = torch.empty((capture, S, W * H * 3 // 2), dtype=torch.uint8, device=dev) if capture and decode else None
 
-    def run_group(n):
+    R_enc = (S // EG) * ((H + 15) // 16)  # MB-row workgroups per encoder launch (h264mi_enc_rows_counter steps)
+
+    def run_group(n, tail=False):
         b = state['g'] % NB
         t0 = state['t']
         for k, (enc, es) in enumerate(zip(encs, ess)):
@@ -574,6 +584,12 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                     outp = None
                     if t0 < capture:  # every frame's picture of the first frames (parity capture, warmup only)
                         outp = [cap_pic[t0 + j, s].data_ptr() if t0 + j < capture else 0 for j in range(n) for s in ss]
+                    if a.recon_gate and not tail:
+                        # frame t0 + j reconstructs once encoder launch t0 + n + j has started all its rows (launch k
+                        # = frame k of this run); only launches this segment will still enqueue
+                        cnt = max(0, min(n, state['seg_end'] - (t0 + n)))
+                        if cnt:
+                            decs[d].set_recon_gate(encs[0].rows_counter(), (t0 + n) * R_enc + int(a.recon_gate_frac * R_enc), R_enc, cnt)
                     decs[d].decode_frames(ptrs, size_ptrs=szp, ready_event=ev_enc[b], out_ptrs=outp)
                 ev_dec[b][d].record(ds)
         if gather is not None:
@@ -591,6 +607,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                 dec.set_streamed(1 if on else a.streamed)
 
     def run_steps(k):
+        state['seg_end'] = state['t'] + k
         # groups of G frames; the last group of a run is decoded frame by frame, so the pipeline drains
         # at frame granularity (each of its frames is entropy-decoded as soon as it is encoded, instead of
         # after the whole group), and those calls reconstruct streamed: the drain is the tail's slowest slice
@@ -601,7 +618,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
             if k <= G and a.tail_frames:
                 set_tail(True)
                 for _ in range(n):
-                    run_group(1)
+                    run_group(1, tail=True)
                 set_tail(False)
             else:
                 run_group(n)
@@ -711,7 +728,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
            'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
-           'streamed_recon': streamed_mode, 'tail_streamed': tail_streamed, 'enc_groups': EG, 'dec_groups': DG,
+           'streamed_recon': streamed_mode, 'tail_streamed': tail_streamed, 'recon_gate': bool(a.recon_gate), 'enc_groups': EG, 'dec_groups': DG,
            'parallelism': f'streams x{world} (weak)'}
     if gather_check is not None:
         selfcheck_ok = selfcheck_ok and gather_check['ok'] is not False

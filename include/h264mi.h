@@ -138,6 +138,12 @@ int h264mi_dec_set_slice_waves(h264mi_decoder *d, int k);
    Returns 0, -1 on a bad argument. h264mi_dec_streamed: the mode in effect. */
 int h264mi_dec_set_streamed(h264mi_decoder *d, int mode);
 int h264mi_dec_streamed(h264mi_decoder *d);
+/* reconstruction gate, for the next decode call only: frame f (< count) of that call is reconstructed once the
+   device uint32 *d_counter has reached target + f * step (wrap-safe comparison), or after limit_us microseconds
+   of waiting -- a scheduling hint, never a correctness condition. With an encoder's rows counter
+   (h264mi_enc_rows_counter) it starts each reconstruction in the tail of a concurrent encoder launch instead of
+   beside its densest part. count 0 clears it. Returns 0, -1 on a bad argument. */
+int h264mi_dec_set_recon_gate(h264mi_decoder *d, const uint32_t *d_counter, uint32_t target, uint32_t step, int count, int limit_us);
 /* automatic streaming's process-wide budget in reconstruction waves (default: a quarter of dec_recon_kernel's
    resident wave slots on the current device, from its CU count and occupancy); waves <= 0 restores the
    default. Applies to later h264mi_dec_set_streamed(-1) / decoder creations. Returns the budget in effect. */
@@ -193,6 +199,10 @@ int h264mi_enc_profile(h264mi_encoder *e, uint64_t *out);
    ticket on the GPU's 100 MHz clock (tickets 0 .. S*mbh-1 MB-row encoders, then the deblocking rows);
    out holds n >= 4 * S * mbh words. -1 when not enabled. */
 int h264mi_enc_timeline(h264mi_encoder *e, uint64_t *out, int n);
+/* the encoder's progress on the device: a uint32 counting the MB-row workgroups its launches have started since
+   creation (S * mbh per frame step; launch k has started all its rows once it reaches (k + 1) * S * mbh).
+   Read-only for callers; for h264mi_dec_set_recon_gate. */
+const uint32_t *h264mi_enc_rows_counter(h264mi_encoder *e);
 const void *h264mi_dec_picture_ptr(h264mi_decoder *d, int stream); /* deblocked picture, coded size (device) */
 int h264mi_dec_coded_size(h264mi_decoder *d, int *cw, int *ch);
 void *h264mi_dec_stream(h264mi_decoder *d);

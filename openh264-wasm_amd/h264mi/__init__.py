@@ -109,6 +109,8 @@ def lib():
             'h264mi_ring_release': (i, [vp, ctypes.c_longlong, vp]),
             'h264mi_ring_stats': (i, [vp, vp, vp, vp, vp]),
             'h264mi_version': (cp, []),
+            'h264mi_enc_rows_counter': (vp, [vp]),
+            'h264mi_dec_set_recon_gate': (i, [vp, vp, ctypes.c_uint32, ctypes.c_uint32, i, i]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -276,6 +278,10 @@ class BatchEncoder:
     def frames_skipped(self, s=0):
         return self._L.h264mi_enc_frames_skipped(self._e, s)
 
+    def rows_counter(self):
+        """device address of the encoder's rows-started counter (h264mi_enc_rows_counter): S * mbh per frame step"""
+        return self._L.h264mi_enc_rows_counter(self._e)
+
     def nal_sizes(self):
         out = (ctypes.c_int * self.S)()
         rc = self._L.h264mi_enc_nal_bytes(self._e, out)
@@ -410,6 +416,12 @@ class BatchDecoder:
         """entropy decoding on CU mask bits [lo, hi) (see h264mi_dec_set_parse_cus)"""
         if self._L.h264mi_dec_set_parse_cus(self._d, lo, hi) != 0:
             raise RuntimeError('h264mi_dec_set_parse_cus failed')
+
+    def set_recon_gate(self, counter, target, step, count, limit_us=4000):
+        """for the next decode call: frame f < count reconstructs once the device uint32 at `counter` reaches
+        target + f * step (h264mi_dec_set_recon_gate; a scheduling hint, bounded by limit_us)"""
+        if self._L.h264mi_dec_set_recon_gate(self._d, counter, target & 0xffffffff, step & 0xffffffff, count, limit_us) != 0:
+            raise RuntimeError('h264mi_dec_set_recon_gate failed')
 
     def set_streamed(self, mode):
         """streamed reconstruction (h264mi_dec_set_streamed): 1 on (the reconstruction stream is kept off the

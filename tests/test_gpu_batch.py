@@ -140,3 +140,45 @@ def test_pipelined_two_stream_decode(gpu_lib, use_event):
         h264mi._hip_memcpy_d2h(a_.ctypes.data, enc.recon_ptr(s), n)
         h264mi._hip_memcpy_d2h(b_.ctypes.data, dec.picture_ptr(s), n)
         assert np.array_equal(a_, b_), f'stream {s}'
+
+
+@pytest.mark.parametrize('mode', ['satisfied', 'timeout'])
+def test_recon_gate(gpu_lib, mode):
+    """h264mi_dec_set_recon_gate is a scheduling hint: a call whose frames wait on an encoder's rows counter
+    (already past the target, or never reaching it: the bounded wait gives up) decodes exactly as an ungated call;
+    the counter advances by S * mbh per encoder frame step"""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    w, h, S, G = 176, 144, 2, 4
+    mbh = (h + 15) // 16
+    gens = [SyntheticStream(20 + s, w, h) for s in range(S)]
+    enc = h264mi.BatchEncoder(w, h, 500000, S)
+    enc.set_frame_skip(False)
+    dec = h264mi.BatchDecoder(w, h, S, max_frames=G)
+    slot = 1 << 20
+    stage = torch.empty((G, S * slot), dtype=torch.uint8, device='cuda')
+    stage_sz = torch.zeros((G, S), dtype=torch.int32, device='cuda')
+    for j in range(G):
+        enc.encode(torch.from_numpy(np.concatenate([g.frame(j) for g in gens])).cuda())
+        enc.copy_nals(stage[j], slot, stage_sz[j])
+    torch.cuda.synchronize()
+    cnt = np.zeros(1, np.uint32)
+    h264mi._hip_memcpy_d2h(cnt.ctypes.data, enc.rows_counter(), 4)
+    assert int(cnt[0]) == G * S * mbh
+    target = 0 if mode == 'satisfied' else G * S * mbh + 1000  # never reached: each frame waits its limit
+    dec.set_recon_gate(enc.rows_counter(), target, S * mbh, G, limit_us=2000)
+    ptrs = [stage.data_ptr() + j * S * slot + s * slot for j in range(G) for s in range(S)]
+    szp = [stage_sz.data_ptr() + 4 * (j * S + s) for j in range(G) for s in range(S)]
+    dec.decode_frames(ptrs, size_ptrs=szp)
+    torch.cuda.synchronize()
+    rc, got = dec.status()
+    assert rc == 0 and all(got)
+    n = dec.cw * dec.ch * 3 // 2
+    for s in range(S):
+        a_, b_ = np.empty(n, np.uint8), np.empty(n, np.uint8)
+        h264mi._hip_memcpy_d2h(a_.ctypes.data, enc.recon_ptr(s), n)
+        h264mi._hip_memcpy_d2h(b_.ctypes.data, dec.picture_ptr(s), n)
+        assert np.array_equal(a_, b_), f'stream {s}'
+    enc.close()
+    dec.close()
