@@ -286,6 +286,22 @@ template <class P> DEV void gran_store2(P base, int idx, uint32_t epoch, uint32_
     gran_store(base + idx + 1, epoch, b);
 #endif
 }
+// Every GPU-side hand-off wait gives up (abort) after H264MI_WAIT_LIMIT_MS of the constant 100 MHz clock,
+// checked every 256 polls (the clock starts at the first check): a time budget rather than a spin count, so
+// contention that slows the polls cannot turn a legitimately long wait into an abort, and the budget does not
+// depend on the poll's latency (round 4: spins > 2^24).
+#ifndef H264MI_WAIT_LIMIT_MS
+#define H264MI_WAIT_LIMIT_MS 2000
+#endif
+struct WaitClock {
+    uint64_t t0 = 0;
+    DEV bool expired() {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) { t0 = t; return false; }
+        return t - t0 > (uint64_t)H264MI_WAIT_LIMIT_MS * 100000u;
+    }
+};
+
 // Wait until the granule at g carries epoch, polling it alone (one 8-byte load, the same address on every
 // lane: one request). gran_wait / DbkSrcGranules use it on the first stale granule of a set instead of
 // re-polling the whole set: a stale poll of a 128-granule record was ~1.3 KB of fabric reads. false on
@@ -294,10 +310,11 @@ template <class P> DEV void gran_store2(P base, int idx, uint32_t epoch, uint32_
 #define H264MI_GRAN_WAIT1 1
 #endif
 template <class P> DEV bool gran_wait1(P g, uint32_t epoch, int32_t *abort_word, unsigned &spins) {
+    WaitClock wc;
     for (;; spins++) {
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ab || spins > (1u << 24)) {
+            if (ab || wc.expired()) {
                 if ((threadIdx.x & 63) == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return false;
             }
@@ -313,6 +330,9 @@ template <class P> DEV bool gran_wait1(P g, uint32_t epoch, int32_t *abort_word,
 template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, int32_t *abort_word) {
     int lane = threadIdx.x & 63;
     uint32_t val = 0;
+#if !H264MI_GRAN_WAIT1
+    WaitClock wc;
+#endif
     for (unsigned spins = 0;; spins++) {
         bool ok = true;
         if (lane < n) {
@@ -327,7 +347,7 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
 #else
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ab || spins > (1u << 24)) {
+            if (ab || wc.expired()) {
                 if (lane == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return false;
             }
@@ -342,11 +362,12 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
 // one granule per lane, already loaded into x (e.g. one step ahead); lanes with need poll it until its
 // tag is epoch. Returns false on abort/timeout.
 template <class P> DEV bool gran_poll(P g, bool need, uint32_t epoch, uint64_t &x, int32_t *abort_word) {
+    WaitClock wc;
     for (unsigned spins = 0;; spins++) {
         if (__all(!need || (uint32_t)(x >> 32) == epoch)) return true;
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ab || spins > (1u << 24)) {
+            if (ab || wc.expired()) {
                 if ((threadIdx.x & 63) == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return false;
             }
