@@ -1,5 +1,7 @@
 """enc_mb_kernel section profile (H264MI_ENC_PROF=1): S streams 1080p IPPP, prints cycles per MB
-per section summed over all waves, for I and P frames.   usage: enc_prof.py [w h br S nf]"""
+per section summed over all waves, for I and P frames. Needs a profiling build of the library loaded with
+H264MI_LIB (the default build compiles the counters out): -DH264MI_ENC_PROF_BUILD, or -DH264MI_ENC_PROF_DETAIL
+for the finer per-wave slots (tools/gpu_prof_rows.sh builds on that one).   usage: enc_prof.py [w h br S nf]"""
 import os, sys
 os.environ['H264MI_ENC_PROF'] = '1'
 import numpy as np
