@@ -2,7 +2,8 @@
 caller waits for each -- scripts/encoder_worker.js:148, scripts/decoder_worker.js:179,189).
 
 usage: capi_latency.py [w h bitrate nframes]  -> one JSON line with per-call ms (median / max) for
-encode_frame_yuv_i420, decode_frame_yuv_i420 and decode_frame_optimized (host buffers, PCIe included).
+encode_frame_yuv_i420, decode_frame_yuv_i420 and decode_frame_optimized (host buffers, PCIe included; frame 0
+excluded as warm-up), and idr_decode_ms: frame 0's IDR decoded again once warm.
 """
 import ctypes, json, os, sys, time
 import numpy as np
@@ -41,9 +42,17 @@ def main(w=1920, h=1080, br=1000000, nf=12):
         if t > 0:  # frame 0 pays one-time allocation
             te.append((t1 - t0) * 1e3); td.append((t3 - t2) * 1e3); tr.append((t4 - t3) * 1e3)
         sizes.append(sz.value)
+        if t == 0:
+            idr = nal
+    # the IDR's single-call decode once warm: frame 0's access unit decoded again (an IDR restarts the stream)
+    t0 = time.perf_counter()
+    L.decode_frame_yuv_i420(0, idr.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(int(idr.size)),
+                            yuv.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ow), ctypes.byref(oh))
+    t_idr = (time.perf_counter() - t0) * 1e3
+    assert (ow.value, oh.value) == (w, h), 'IDR re-decode gave no picture'
     st = lambda v: {'median_ms': round(float(np.median(v)), 3), 'max_ms': round(float(np.max(v)), 3)}
     print(json.dumps({'width': w, 'height': h, 'bitrate': br, 'frames': nf, 'nal_bytes': sizes,
-                      'encode_frame_yuv_i420': st(te), 'decode_frame_yuv_i420': st(td), 'decode_frame_optimized': st(tr),
+                      'idr_decode_ms': round(t_idr, 3), 'encode_frame_yuv_i420': st(te), 'decode_frame_yuv_i420': st(td), 'decode_frame_optimized': st(tr),
                       'note': 'host buffers in and out (PCIe included), one frame per call, caller waits'}))
 
 

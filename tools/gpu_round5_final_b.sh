@@ -18,3 +18,7 @@ H264MI_LIB=openh264-wasm_amd/lib/libh264mi_detail.so ./tools/gpu_prof_rows.sh fi
 mv gpurun_out/r5final5_detail_encprof_s32*.txt $d/ 2>/dev/null
 timeout -k 10 200 python -u tools/enc_timeline.py 1920 1080 1000000 32 6 > $d/timeline_s32.txt 2>&1 || exit $?
 grep "frame 4" -A3 $d/timeline_s32.txt | cut -c1-200
+for br in 1000000 8000000; do
+  timeout -k 10 240 python -u tools/capi_latency.py 1920 1080 $br 12 > $d/capi_$br.json 2> $d/capi_$br.err || { tail -5 $d/capi_$br.err; exit 1; }
+  tail -c 300 $d/capi_$br.json
+done
