@@ -78,8 +78,8 @@ def parse():
     ap.add_argument('--parse-streams', type=int, default=3, help='HIP streams the decoder rotates entropy decoding over')
     ap.add_argument('--parse-cus', type=int, default=-1,
                     help='CUs reserved for entropy decoding (CU mask bits [0, n) for the parse streams, the rest for the '
-                         'encoder / reconstruction streams); 0 = shared; default when encoding and decoding: 32 for >= 128 '
-                         'slices per call, else 24; 0 for decode-only')
+                         'encoder / reconstruction streams); 0 = shared; default when encoding and decoding: 20 per 128 '
+                         'slices per call (>= 128), else 24; 0 for decode-only')
     ap.add_argument('--recon-cus', type=int, default=0,
                     help='CUs reserved for the reconstruction stream (mask bits [parse_cus, parse_cus + n)); the encoder '
                          'keeps the rest. 0 = reconstruction shares the encoder\'s CUs')
@@ -108,9 +108,13 @@ def parse():
     # 3738-3902 frames/s over 8 runs, profiles/round4/ab_enc_groups*.txt) and halve the per-launch roofline
     a.enc_groups = a.enc_groups or 1
     if a.parse_cus < 0:  # a reserved decode lane pays only beside the encoder's wavefronts
-        # a slice wave takes a quarter of a CU's LDS (four per CU): 32 CUs hold the 128 slices of a
-        # 32-stream, 4-frame call at once (24 CUs: two rounds); 40 measured slower (profiles/round3/pcus2)
-        a.parse_cus = (32 if a.streams * a.group >= 128 else 24) if a.config in (0, 3, 5) else 0
+        # a slice wave takes a quarter of a CU's LDS (four per CU). Round 5, after the reconstruction's
+        # latency work (profiles/round5/sweep_parse_cus_final.txt): the 128 slices of a 32-stream, 4-frame call
+        # run best on the fewest CUs that take them in two rounds -- 16 CUs 4517-4546 frames/s, 20 4512-4521,
+        # 24 4501, 32 4485-4492, 40 4211-4230; 12 and 8 (three and four rounds) drop to 3655. 20 keeps a round's
+        # margin: 20 CUs per 128 slices, in steps of 4 (smaller calls keep the earlier 24)
+        sl = a.streams * a.group
+        a.parse_cus = (-(-sl * 20 // (128 * 4)) * 4 if sl >= 128 else 24) if a.config in (0, 3, 5) else 0
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
