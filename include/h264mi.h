@@ -97,6 +97,13 @@ const void *h264mi_enc_recon_ptr(h264mi_encoder *e, int stream);   /* deblocked 
 const void *h264mi_enc_input_buffer(h264mi_encoder *e);            /* internal device input area (nstreams frames) */
 size_t h264mi_enc_frame_bytes(h264mi_encoder *e);
 int h264mi_enc_last_qp(h264mi_encoder *e, int stream);
+/* the rate control's state after the last frame step (RC_BITRATE_MODE restated from h264.wasm),
+   16 int32 in the oracle's h264o_enc_rc_state order: {skipped, QP, average QP, target bits, remaining bits,
+   buffer fullness, continual skips, frame complexity, min / max frame QP, bits per frame, P frames, IDRs,
+   skip flag, remaining weights, frames coded in the VGOP} */
+int h264mi_enc_rc_state(h264mi_encoder *e, int stream, int *out16);
+/* RcConvertQStep2Qp as the device computes it (thresholds; the wasm's musl-logf form is the oracle's) */
+int h264mi_rc_qstep_to_qp(int qstep);
 int h264mi_enc_mbinfo(h264mi_encoder *e, int stream, void *host_out); /* 128 B per MB (h264mi_types.h MbInfo) */
 void *h264mi_enc_stream(h264mi_encoder *e);
 const int *h264mi_enc_nal_size_dev(h264mi_encoder *e, int stream); /* device address of the NAL byte count */

@@ -40,6 +40,20 @@ __constant__ const uint8_t c_CHROMA_QP[52] = {
 __constant__ const uint8_t c_LAMBDA[52] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 4,
                                            5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 23, 25, 29, 32, 36, 40, 45, 51, 57, 64, 72, 81, 91};
 
+// Rate control: OpenH264's g_kiQpToQstepTable (h264.wasm linear address 43696, pinned by
+// tests/golden/openh264_tables.json "rc_qstep"), and RcConvertQStep2Qp as thresholds: QP k >= 1 for a QStep at or
+// above THR[k - 1]. The wasm computes trunc(6 * logf(QStep / 100.0f) / ln 2 + 4.5) with musl's logf (func 483);
+// tests/test_rc.py checks these thresholds against the oracle's restatement of that function over every QStep up
+// to 400000. QPs above 52 are never used: every result is clipped into the camera range [12, 42].
+#define H264MI_RC_QSTEP_LIST 63, 71, 79, 89, 100, 112, 126, 141, 159, 178, 200, 224, 252, 283, 317, 356, 400, 449, 504, \
+    566, 635, 713, 800, 898, 1008, 1131, 1270, 1425, 1600, 1796, 2016, 2263, 2540, 2851, 3200, 3592, 4032, 4525, 5080, \
+    5702, 6400, 7184, 8063, 9051, 10159, 11404, 12800, 14368, 16127, 18102, 20319, 22807
+#define H264MI_RC_QP_THR_LIST 67, 75, 85, 95, 106, 119, 134, 150, 169, 189, 212, 238, 267, 300, 337, 378, 424, 476, 534, \
+    600, 673, 756, 848, 952, 1068, 1199, 1346, 1511, 1696, 1903, 2136, 2398, 2691, 3021, 3391, 3806, 4272, 4795, 5382, \
+    6041, 6781, 7611, 8543, 9590, 10764, 12082, 13562, 15222, 17086, 19179, 21527, 24164
+__constant__ const int32_t c_RC_QSTEP[52] = {H264MI_RC_QSTEP_LIST};
+__constant__ const int32_t c_RC_QP_THR[52] = {H264MI_RC_QP_THR_LIST};
+
 DEV int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 DEV int clip1(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 // Clip1(x >> s) for byte-packed results. Clamp-first form: hipcc (ROCm 7.2, gfx950) selects

@@ -48,10 +48,37 @@ struct MbCoef {
 };
 static_assert(sizeof(MbCoef) == 832, "MbCoef layout");
 
+// OpenH264's RC_BITRATE_MODE state of one stream, restated from the reference's h264.wasm
+// (the oracle's Rc in oracle/h264o_enc.c follows the same functions; field comments name the wasm struct
+// offsets: rc+N SWelsSvcRc, tl+N its SRCTemporal[0]). The host sets the constants at creation
+// (RcInitSequenceParameter, RcInitTlWeight, RcUpdateBitrateFps, RcCalculateIdrQp's table part);
+// enc_begin_kernel makes the skip decision and the picture init, enc_pack_kernel the picture update.
+struct RcState {
+    // constants
+    int32_t nmb, mbw, mb_per_gom, gom_count;  // rc+156, rc+160 iNumberMbGom, rc+164 iGomSize
+    int32_t skip_qp;                          // rc+188 iSkipQpValue
+    int32_t c_bpf, c_min_bits_tl, c_max_bits_tl, c_buffer_size_skip;  // RcUpdateBitrateFps's results
+    int32_t tl_weight, gop_num;               // tl+8, rc+180
+    int32_t idr_lo, idr_hi, idr_table_qp;     // RcCalculateIdrQp: QP range (clipped) and the first IDR's table QP
+    int32_t skip_en;                          // bEnableFrameSkip
+    // state
+    int32_t skip_flag, continual_skip;        // rc+280, rc+284
+    int32_t bpf, min_bits_tl, max_bits_tl, buffer_size_skip;  // rc+40, tl+0, tl+4, rc+228 (set at the first IDR)
+    int32_t remaining, vgop_bits, remaining_weights, gop_index, frame_coded_in_vgop;  // rc+60, +56, +112, +184, +172
+    int32_t target, bits_level;               // rc+68, rc+72
+    int32_t init_qp, last_qscale, qstep, avg_qp, min_frame_qp, max_frame_qp;  // rc+8, +224, +212, +144, +148, +152
+    int32_t idr_num, intra_mb_count, pframe_num;  // rc+76, rc+88, tl+24
+    int32_t prev_idx;                         // which psrc holds the last coded frame's luma
+    int32_t pad0;
+    int64_t fullness;                         // rc+232
+    int64_t intra_cmplx, intra_cmplx_mean;    // rc+80, rc+96
+    int64_t linear_cmplx, frame_cmplx_mean;   // tl+16, tl+32
+    int64_t frame_cmplx;                      // the frame's iFrameComplexity (enc_cmplx_kernel's GOM values)
+};
+
 // Per-stream encoder state (device resident; read/updated by the frame-begin and pack kernels).
 struct EncState {
-    int32_t qp;            // QP for the next frame (rate control output)
-    int32_t cur_qp;        // QP of the frame being coded
+    int32_t cur_qp;        // QP of the frame being coded (iGlobalQp: slice QP)
     int32_t cur_idr;       // 1 if the frame being coded is IDR
     int32_t force_idr;     // host request (force_key_frame)
     int32_t first;         // no frame coded yet
@@ -60,18 +87,13 @@ struct EncState {
     int32_t bitrate;
     int32_t nal_bytes;     // bytes of the last coded frame (all NAL units, start codes included)
     int32_t err;           // nonzero: a kernel detected an error / timeout
-    int64_t last_bits;
-    int64_t vbuf;          // rate control: virtual buffer fullness in bits
     int32_t cur_skip;      // 1 if the frame being coded is skipped by the rate control (0 bytes out)
-    int32_t skip_en;       // frame skipping enabled (the wrapper's default)
     int32_t skipped;       // frames skipped so far
     int32_t inject_err;    // test hook (h264mi_enc_inject_error): the next coded frame fails with this code
                            // (3: through the RBSP-overflow branch of enc_pack_kernel)
-    // rate control state beside qp (oracle rc_frame_qp): the first IDR's table QP and
-    // the IDR QP range (RcCalculateIdrQp), IDRs / P frames coded, the coded frame's QP window
-    int32_t init_qp, rmin, rmax, idr_num, pframes, cur_qmin, cur_qmax;
     int32_t sps_bytes, pps_bytes;
     uint8_t sps[64], pps[32];
+    RcState rc;
 };
 
 // Per-stream encoder buffers for one frame step.
@@ -100,6 +122,9 @@ struct EncDesc {
     int32_t *rowqp;         // MB-row (GOM) QP offsets of the frame being coded (written by the previous pack)
     int32_t *rowbits;       // macroblock_layer() bits per MB row of the last coded frame
     uint64_t *rowq;         // per MB row: {epoch, QPY entering the row} granules (row r publishes r + 1)
+    uint8_t *psrc[2];       // coded-size luma of the last coded frame and of the frame being coded (RcState::prev_idx):
+                            // the preprocessing's reference picture for the frame complexity (enc_cmplx_kernel)
+    uint32_t *gomc;         // per GOM: [0, G) SAD against the last coded source (P), [G, 2G) variance (I)
 };
 
 // One stream's padded reference planes and the picture they are built from (enc_planes.inc).

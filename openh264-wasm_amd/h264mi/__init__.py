@@ -55,6 +55,8 @@ def lib():
             'h264mi_enc_input_buffer': (vp, [vp]),
             'h264mi_enc_frame_bytes': (ctypes.c_size_t, [vp]),
             'h264mi_enc_last_qp': (i, [vp, i]),
+            'h264mi_enc_rc_state': (i, [vp, i, vp]),
+            'h264mi_rc_qstep_to_qp': (i, [i]),
             'h264mi_enc_mbinfo': (i, [vp, i, vp]),
             'h264mi_enc_ref_planes': (i, [vp, i, vp]),
             'h264mi_enc_stream': (vp, [vp]),
@@ -326,6 +328,16 @@ class BatchEncoder:
 
     def last_qp(self, s=0):
         return self._L.h264mi_enc_last_qp(self._e, s)
+
+    RC_FIELDS = ('skipped', 'qp', 'avg_qp', 'target', 'remaining', 'fullness', 'continual', 'cmplx', 'min_qp',
+                 'max_qp', 'bpf', 'pframes', 'idrs', 'skip_flag', 'remaining_weights', 'coded_in_vgop')
+
+    def rc_state(self, s=0):
+        """stream s's rate-control state after the last frame step (h264mi_enc_rc_state)"""
+        out = (ctypes.c_int * 16)()
+        if self._L.h264mi_enc_rc_state(self._e, s, out) != 0:
+            raise RuntimeError('h264mi_enc_rc_state failed')
+        return dict(zip(self.RC_FIELDS, list(out)))
 
     def close(self):
         if self._e:

@@ -38,7 +38,11 @@ int h264o_rc_init_qp(int w, int h, int bitrate);
 int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax);  /* first IDR QP, IDR QP range */
 void h264o_rc_constants(int32_t out[8]);  /* fps, QP min/max, frame window lower/upper, IDR window, IDR ratio, skip ratio */
 int h264o_table(const char *name, double *out);  /* the oracle's copy of an OpenH264 table (entry count, -1 unknown) */
-int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr);
+/* OpenH264's rate control restated from h264.wasm */
+float h264o_logf(float x);                 /* musl logf (func 483) */
+int h264o_rc_qstep2qp(int32_t qstep);      /* RcConvertQStep2Qp */
+void h264o_enc_set_gom_exact(H264OEnc *e, int enable);  /* MB QPs by OpenH264's GOM rule (funcs 1215 / 1206) */
+void h264o_enc_rc_state(const H264OEnc *e, int32_t out[16]);
 size_t h264o_write_sps(int w, int h, int bitrate, uint8_t *out);
 int h264o_level_idc(int w, int h, int bitrate, int *cs3);
 size_t h264o_write_pps(uint8_t *out);

@@ -22,9 +22,12 @@
 #define RC_FPS 60           /* GetDefaultParams fMaxFrameRate (wasm func 1023); the wrapper never sets it */
 #define QP_MIN 12           /* iMinQp / iMaxQp for camera content when the caller leaves iMinQp 0 (func 597) */
 #define QP_MAX 42
-#define FRAME_DQP_LOWER 3   /* iFrameDeltaQpLower / iFrameDeltaQpUpper at iRcVaryRatio 0 (func 592) */
-#define FRAME_DQP_UPPER 5
+#define RC_VARY 10          /* iRcVaryPercentage = iRcVaryRatio (InitializeExt default, func 1021) */
+#define FRAME_DQP_LOWER (RC_VARY / -100 + 3)  /* iFrameDeltaQpLower / Upper (RcInitSequenceParameter, func 592) */
+#define FRAME_DQP_UPPER (RC_VARY / -50 + 5)
 #define IDR_QP_WINDOW 3     /* RcCalculateIdrQp: the IDR's frame QP window (func 1226) */
+#define VGOP_SIZE 8         /* RcInitVGop / RcInitTlWeight: iGopNumberInVGop = 8 >> iDecompositionStages */
+#define WEIGHT_MULTIPLY 2000
 /* Stream syntax OpenH264 writes at the wrapper's parameters, read from the same binary's code
  * (tools/wasm_syntax.py pins each instruction): WelsInitSps (func 280) stores
  * uiLog2MaxFrameNum 15 and uiPocType 2 as one i64 constant (file offset 167929), so the slice header
@@ -35,41 +38,122 @@
 #define CROSS_THR 1024  /* cross search when the best integer cost exceeds this */
 #endif
 
+/* OpenH264's RC_BITRATE_MODE state at the wrapper's parameters (one spatial and one temporal layer, one
+ * slice), restated from the reference's h264.wasm. Field comments name the wasm struct offsets the
+ * functions below follow: rc+N = SWelsSvcRc (336 bytes per layer), tl+N = its SRCTemporal[0] (48 bytes),
+ * sl+N = the slice's SRCSlicing; DESIGN.md §3.6 lists the functions. */
+typedef struct {
+    /* sequence (RcInitSequenceParameter inlined in func 592 @401199-401452; RcInitTlWeight func 702;
+     * RcUpdateBitrateFps func 697) */
+    int mbw, nmb, mb_per_gom, gom_count;  /* rc+156 iNumberMbFrame, rc+160 iNumberMbGom, rc+164 iGomSize */
+    int skip_qp;            /* rc+188 iSkipQpValue */
+    int bitrate, max_bitrate;
+    int bpf, max_bpf;       /* rc+40 iBitsPerFrame, rc+44 iMaxBitsPerFrame */
+    int min_bits_tl, max_bits_tl;  /* tl+0, tl+4 */
+    int buffer_size_skip;   /* rc+228 */
+    int tl_weight, gop_num; /* tl+8 iTlayerWeight, rc+180 iGopNumberInVGop */
+    int skip_en;            /* param bEnableFrameSkip */
+    /* frame skipping (func 589's check, CheckFrameSkipBasedMaxbr func 1258, WelsRcPostFrameSkipping func 1254) */
+    int skip_flag;          /* rc+280 bSkipFlag */
+    int continual_skip;     /* rc+284 iContinualSkipFrames */
+    int skip_frame_num, skip_in_vgop;  /* rc+168, rc+176 */
+    int64_t fullness;       /* rc+232 iBufferFullnessSkip */
+    /* VGOP bit allocation (RcInitVGop, RcDecideTargetBits; func 1226) */
+    int remaining;          /* rc+60 iRemainingBits */
+    int vgop_bits;          /* rc+56: the VGOP's starting budget (bFixRCOverShoot) */
+    int remaining_weights;  /* rc+112 */
+    int gop_index;          /* rc+184 iGopIndexInVGop */
+    int frame_coded_in_vgop;/* rc+172 */
+    int gop_bits_dq;        /* tl+12 */
+    int target;             /* rc+68 iTargetBits */
+    int bits_level;         /* rc+72 iCurrentBitsLevel (2 = BITS_EXCEEDED) */
+    /* QP (RcCalculateIdrQp / RcCalculatePictureQp, func 1226) */
+    int init_qp;            /* rc+8 iInitialQp */
+    int global_qp;          /* ctx+244 iGlobalQp: slice QP, the first GOM's QP */
+    int last_qscale;        /* rc+224 iLastCalculatedQScale */
+    int qstep;              /* rc+212 iQStep */
+    int avg_qp;             /* rc+144 iAverageFrameQp */
+    int min_frame_qp, max_frame_qp;  /* rc+148, rc+152 */
+    /* R-Q models (RcUpdateIntraComplexity, RcUpdateFrameComplexity func 676) */
+    int idr_num, intra_mb_count;     /* rc+76, rc+88 */
+    int64_t intra_cmplx, intra_cmplx_mean;  /* rc+80, rc+96 */
+    int pframe_num;                  /* tl+24 */
+    int64_t linear_cmplx, frame_cmplx_mean;  /* tl+16, tl+32 */
+    int64_t frame_cmplx;    /* the preprocessing's iFrameComplexity of the frame being coded (rc_complexity) */
+    /* GOM (WelsRcMbInitGom func 1215, WelsRcMbInfoUpdateGom func 1206): exact mode only */
+    int bits_per_mb;        /* rc+64 iBitsPerMb */
+    int target_bits_slice, frame_bits_slice, gom_bits_slice, gom_target_bits;  /* sl+1372, +1380, +1384, +1388 */
+    int complexity_index, calc_qp;   /* sl+1348 iComplexityIndexSlice, sl+1352 iCalculatedQpSlice */
+    int total_qp, total_mb;          /* sl+1364, sl+1368 */
+    uint32_t *gom_sad;      /* rc+132 pCurrentFrameGomSad: the frame's complexity per GOM */
+} Rc;
+
 struct H264OEnc {
     int w, h, mbw, mbh, cw, ch;
     int bitrate;
     uint8_t *src[3], *rec[3], *ref[3];
+    uint8_t *prev_src;  /* luma source of the last coded frame, coded size (the preprocessing's reference picture) */
     MBInfo *mbs;
     int first, force_idr;
     int frame_num, idr_pic_id, poc;
-    int qp;           /* the next frame's QP before its bounds (the bits-ratio step below) */
     int last_qp, last_idr;
-    int init_qp, rmin, rmax;  /* RcCalculateIdrQp: first IDR QP and the IDR QP range */
-    int idr_num, pframes;     /* IDRs / P frames coded (OpenH264 iIdrNum, iPFrameNum) */
-    int qmin, qmax;           /* the coded frame's QP window (iMinFrameQp, iMaxFrameQp): clamps the row QPs */
-    int64_t last_bits;
-    /* GOM (MB-row) rate control and frame skipping */
+    Rc rc;
+    int gom_exact;    /* MB QPs by OpenH264's GOM rule (h264o_enc_set_gom_exact); else this project's row plan */
+    /* this project's MB-row QP plan of P frames */
     int *rowqp;       /* QP offset plan of the next frame, one per MB row (added to the frame QP) */
     int64_t *rowbits; /* macroblock_layer() bits per MB row of the last coded frame */
-    int64_t vbuf;     /* virtual buffer fullness (bits) */
-    int skip_en, skipped;
+    int skipped, last_skipped;
     int stat_cross, stat_cross_moved, stat_nb_start;  /* ME path counters (tests: coverage of the search stages) */
 };
 
 /* ---------------- rate control ---------------- */
-/* RcCalculateIdrQp restated from the reference's h264.wasm (func 1226, file offsets 766934-767578):
- * bits per pixel = bitrate / (float)(fps * w * h); area class by w * h; the first column i of
- * OH_RC_BPP[class] at or above it (the search starts at column 0: bFixRCOverShoot defaults to 1);
- * IDR QP range = OH_RC_QP_RANGE[i] clipped to [QP_MIN, QP_MAX]; first IDR QP = OH_RC_INIT_QP[class][i]
- * clipped to that range. Writes *rmin / *rmax, returns the first IDR QP. */
-int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax) {
-    float p = (float)RC_FPS * (float)w;
-    p = p * (float)h;
-    const double bpp = (double)bitrate / (double)p;
-    const int area = w * h;
-    const int cls = area < 28801 ? 0 : (area < 115201 ? 1 : (area < 460801 ? 2 : 3));
+/* musl logf as h264.wasm func 483 computes it (RcConvertQStep2Qp's log): table-driven, in double, no FMA
+ * (oracle/Makefile builds with -ffp-contract=off) */
+float h264o_logf(float x) {
+    uint32_t ix;
+    memcpy(&ix, &x, 4);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x7f800000u <= 0x807fffffu) {  /* 0, subnormal, negative, inf, nan */
+        if ((ix << 1) == 0) return -1.0f / 0.0f;
+        if (ix == 0x7f800000u) return x;
+        if (!((ix << 1) < 0xff000000u && (int32_t)ix >= 0)) return (x - x) / (x - x);
+        const float xs = x * 8388608.0f;
+        memcpy(&ix, &xs, 4);
+        ix -= 192937984u;  /* 23 << 23 */
+    }
+    const uint32_t tmp = ix - 1060306944u;  /* 0x3f330000 */
+    const int i = (int)((tmp >> 19) & 15), k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    float fz;
+    memcpy(&fz, &iz, 4);
+    const double r = (double)fz * OH_LOGF_T[i][0] + -1.0, r2 = r * r;
+    return (float)(((OH_LOGF_P[1] * r2) + ((OH_LOGF_P[2] * r) + OH_LOGF_P[3])) * r2 +
+                   ((((double)k * OH_LOGF_P[0]) + OH_LOGF_T[i][1]) + r));
+}
+/* RcConvertQStep2Qp (inlined twice in func 1226, 767413-767467 / 767927-767980): QP 0 below QStep 64,
+ * else trunc(6 * logf(QStep / 100.0f) / ln 2 + 4 + 0.5) */
+int h264o_rc_qstep2qp(int32_t qstep) {
+    if (qstep < 64) return 0;
+    const float t = h264o_logf((float)(uint32_t)qstep / 100.0f);
+    return (int)((((double)(t * 6.0f)) / 0.6931471805599453 + 4.0) + 0.5);
+}
+/* bits per pixel class and column of RcCalculateIdrQp (func 1226, 766870-767222): the layer's size is the
+ * picture rounded up to whole MBs (ParamTranscode, func 585, 373611-373776), bpp = bitrate / (float)(fps * w * h),
+ * the first column at or above it from column 0 (bFixRCOverShoot) */
+static void rc_idr_class(int w, int h, int bitrate, int *cls, int *col) {
+    const int w16 = (w + 15) & ~15, h16 = (h + 15) & ~15;
+    const float fps = (float)RC_FPS;
+    const double bpp = (double)bitrate / (double)((fps * (float)w16) * (float)h16);
+    const int area = w16 * h16;
+    *cls = area < 28801 ? 0 : ((unsigned)area < 115201u ? 1 : ((unsigned)area < 460801u ? 2 : 3));
     int i = 0;
-    while (i < 4 && !(OH_RC_BPP[cls][i] >= bpp)) i++;
+    while (i < 4 && !(OH_RC_BPP[*cls][i] >= bpp)) i++;
+    *col = i;
+}
+/* the first IDR's QP and the IDR QP range {*rmin, *rmax} */
+int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax) {
+    int cls, i;
+    rc_idr_class(w, h, bitrate, &cls, &i);
     const int mx = clip3(QP_MIN, QP_MAX, OH_RC_QP_RANGE[i][0]), mn = clip3(QP_MIN, QP_MAX, OH_RC_QP_RANGE[i][1]);
     *rmin = mn; *rmax = mx;
     return clip3(mn, mx, OH_RC_INIT_QP[cls][i]);
@@ -78,46 +162,268 @@ int h264o_rc_init_qp(int w, int h, int bitrate) {
     int a, b;
     return h264o_rc_idr_params(w, h, bitrate, &a, &b);
 }
-/* The next frame's QP before its bounds: this project's step on the bits of the frame just coded
- * against the per-frame target T = bitrate / fps (x4 for an IDR: iIdrBitrateRatio 400). OpenH264
- * derives it from its complexity model instead (RcCalculatePictureQp); not pinned. */
-int h264o_rc_next_qp(int qp, int64_t bits, int bitrate, int was_idr) {
-    int64_t T = bitrate / RC_FPS;
-    if (was_idr) T *= 4;
-    int d;
-    if (bits > 2 * T) d = 3;
-    else if (2 * bits > 3 * T) d = 2;
-    else if (100 * bits > 115 * T) d = 1;
-    else if (2 * bits < T) d = -2;
-    else if (100 * bits < 85 * T) d = -1;
-    else d = 0;
-    return clip3(QP_MIN, QP_MAX, qp + d);
+/* RcInitSequenceParameter (func 592, 401199-401452) at creation; RcInitTlWeight / RcUpdateBitrateFps run at the
+ * first IDR. The maximum bitrate is WelsBitRateVerification's (func 278): the caller leaves it unspecified and
+ * uiLevelIdc unknown, so it becomes level 5.2's MaxBR x 1200. */
+static void rc_init(Rc *rc, int w, int h, int bitrate) {
+    uint32_t *g = rc->gom_sad;
+    memset(rc, 0, sizeof(*rc));
+    const int w16 = (w + 15) & ~15, h16 = (h + 15) & ~15;
+    rc->mbw = w16 >> 4;
+    rc->nmb = rc->mbw * (h16 >> 4);
+    const int narrow = rc->mbw < 31, g0 = narrow ? 1 : 2, g1 = narrow ? 2 : 4;
+    rc->skip_qp = narrow ? 24 : 31;
+    rc->mb_per_gom = rc->mbw * ((RC_VARY * (g1 - g0)) / 100 + g0);
+    rc->gom_count = (rc->mb_per_gom + rc->nmb - 1) / rc->mb_per_gom;
+    rc->bitrate = bitrate;
+    rc->max_bitrate = 0;
+    for (int i = 0; i < 17; i++) if (OH_LEVEL_LIMITS[i][0] == 52) rc->max_bitrate = OH_LEVEL_LIMITS[i][4] * 1200;
+    rc->skip_en = 1;
+    rc->gom_sad = g;
 }
-/* The coded frame's QP and window (RcCalculateIdrQp / RcCalculatePictureQp, wasm func 1226):
- * IDR: the first takes the table QP, later ones the step result, clipped to the IDR range; window
- * QP -/+ IDR_QP_WINDOW inside the range. P: the first P frame takes the first IDR's QP, later ones
- * the step result; window [last - FRAME_DQP_LOWER, last + FRAME_DQP_UPPER] inside [QP_MIN, QP_MAX],
- * last = the previous coded frame's QP; the QP is clipped to the window. */
-static int rc_frame_qp(H264OEnc *e, int idr) {
-    int q;
-    if (idr) {
-        q = e->idr_num == 0 ? e->init_qp : clip3(e->rmin, e->rmax, e->qp);
-        e->qmin = clip3(e->rmin, e->rmax, q - IDR_QP_WINDOW);
-        e->qmax = clip3(e->rmin, e->rmax, q + IDR_QP_WINDOW);
-        e->idr_num++;
-    } else {
-        q = e->pframes == 0 ? e->init_qp : e->qp;
-        e->qmin = clip3(QP_MIN, QP_MAX, e->last_qp - FRAME_DQP_LOWER);
-        e->qmax = clip3(QP_MIN, QP_MAX, e->last_qp + FRAME_DQP_UPPER);
-        q = clip3(e->qmin, e->qmax, q);
-        e->pframes++;
+/* RcUpdateBitrateFps (func 697): float per-frame bits at the 60 fps default, the temporal layer's bit bounds
+ * (55 % / 150 % of the GOP's bits at iRcVaryRatio 10, weighted), the skip buffer (50 % of the bitrate) */
+static void rc_update_bitrate_fps(Rc *rc) {
+    const float fps = (float)RC_FPS;
+    const int in_bpf = (int)((fps * 0.5f + (float)rc->bitrate) / fps);
+    const int64_t gop_bits = in_bpf;  /* << iDecompositionStages (0) */
+    rc->max_bits_tl = (int)((gop_bits * 150 * rc->tl_weight + 100000) / 200000);
+    rc->min_bits_tl = (int)((gop_bits * (100 - ((100 - RC_VARY) >> 1)) * rc->tl_weight + 100000) / 200000);
+    rc->buffer_size_skip = (int)((50 * (int64_t)rc->bitrate + 50) / 100);
+    if (rc->bpf >= 2)
+        rc->remaining = (int)(((int64_t)((uint32_t)rc->bpf >> 1) + (int64_t)rc->remaining * in_bpf) / (int64_t)(uint32_t)rc->bpf);
+    rc->bpf = in_bpf;
+    rc->max_bpf = (int)((fps * 0.5f + (float)rc->max_bitrate) / fps);
+}
+/* RcInitVGop with bFixRCOverShoot (func 1226, 764341-764437 / 765012-765094 / 765431-765497): an overspent VGOP
+ * carries its deficit into the next, an underspent one does not carry its surplus */
+static void rc_init_vgop(Rc *rc) {
+    const int t = rc->remaining + (rc->gop_index - rc->gop_num) * (rc->vgop_bits / rc->gop_num);
+    rc->remaining = (t < 0 ? t : 0) + (rc->bpf << 3);
+    rc->vgop_bits = rc->remaining;
+    rc->gop_index = 0;
+    rc->frame_coded_in_vgop = 0;
+    rc->remaining_weights = rc->gop_num * WEIGHT_MULTIPLY;
+    rc->gop_bits_dq = 0;
+    rc->skip_in_vgop = 0;
+}
+static int64_t cmplx_ratio(int64_t fc, int64_t mean) {  /* WELS_DIV_ROUND64(fc * 100, mean) clipped to 80..120 */
+    int64_t r = mean == 0 ? fc * 100 : (fc * 100 + mean / 2) / mean;
+    r = r <= 80 ? 80 : r;
+    return r >= 120 ? 120 : r;
+}
+static int32_t qstep_model(int64_t cmplx, int64_t ratio, int target) {  /* WELS_DIV_ROUND64(cmplx * ratio, target * 100) */
+    const int64_t v = target == 0 ? cmplx * ratio : ((int64_t)(target * 50) + cmplx * ratio) / (int64_t)(target * 100);
+    return (int32_t)(uint32_t)(uint64_t)v;
+}
+/* Frame skip decision before a frame (WelsEncoderEncodeExt's check, func 589 376000-376503): a flag left by the
+ * last update skips at once; otherwise CheckFrameSkipBasedMaxbr (func 1258) skips while the buffer holds more than
+ * its size and the run of skipped frames is at most (round(fullness / bits per frame) + 1) >> 1. Its three
+ * maximum-bitrate cases need iCheckWindowInterval > 2500 ms, which the wrapper's zero timestamps never reach
+ * (UpdateMaxBrCheckWindowStatus, func 1251). bFixRCOverShoot: 1258 only sets the flag (774599-774612).
+ * Returns 1 when the frame is skipped unless it is an IDR. */
+static int rc_judge_skip(Rc *rc) {
+    if (!rc->skip_flag) {
+        if (!rc->skip_en) return 0;
+        const int64_t r = rc->bpf == 0 ? rc->fullness : (rc->fullness + rc->bpf / 2) / rc->bpf;
+        const int pred_tar = ((int32_t)(uint32_t)(uint64_t)r + 1) >> 1;
+        rc->skip_flag = pred_tar >= rc->continual_skip && rc->fullness > rc->buffer_size_skip;
+        if (!rc->skip_flag) return 0;
     }
-    return q;
+    rc->skip_flag = 0;
+    rc->continual_skip++;
+    return 1;
 }
-/* MB-row ("GOM") QP offsets of the next frame: rows that cost more than the mean in the last coded
- * frame are quantised more coarsely, cheaper rows more finely; the row QP is the frame QP plus the
- * offset, clipped to the frame's window (this project's rule; OpenH264 re-plans GOMs from the bits
- * of the frame being coded, a serial dependency). */
+/* WelsRcPostFrameSkipping (func 1254): the skipped frame's bits leave the buffer and return to the VGOP */
+static void rc_post_skip(Rc *rc) {
+    rc->fullness -= rc->bpf;
+    rc->remaining += rc->bpf;
+    rc->skip_frame_num++;
+    rc->skip_in_vgop++;
+    if (rc->fullness < 0) rc->fullness = 0;
+}
+/* WelsRcPictureInitGom (func 1226) for a coded frame: RcInitRefreshParameter at the first IDR, RcUpdateTemporalZero,
+ * RcDecideTargetBits, RcCalculateIdrQp / RcCalculatePictureQp, RcInitSliceInformation, RcInitGomParameters and the
+ * slice's RC init (func 225, 120355-120428). rc->frame_cmplx holds the frame's complexity. */
+static void rc_picture_init(Rc *rc, int idr, int w, int h) {
+    rc->continual_skip = 0;
+    if (idr && rc->idr_num == 0) {  /* RcInitRefreshParameter (763796-764694) */
+        rc->intra_cmplx = 0; rc->intra_mb_count = 0; rc->intra_cmplx_mean = 0;
+        rc->pframe_num = 0; rc->linear_cmplx = 0; rc->frame_cmplx_mean = 0;
+        rc->fullness = 0; rc->gop_index = 0; rc->vgop_bits = 0;
+        rc->bpf = 0; rc->remaining = 0;
+        rc->tl_weight = OH_RC_TL_WEIGHT[0][0];  /* RcInitTlWeight: one temporal layer, decomposition stages 0 */
+        rc->gop_num = VGOP_SIZE >> 0;
+        rc_update_bitrate_fps(rc);
+        rc_init_vgop(rc);
+    }
+    /* RcUpdateTemporalZero (764840-765777): a new VGOP after iGopNumberInVGop frames and at every IDR */
+    if (rc->gop_index == rc->gop_num || idr) rc_init_vgop(rc);
+    rc->gop_index++;
+    /* RcDecideTargetBits (766402-766725) */
+    rc->bits_level = 0;
+    if (idr) rc->target = rc->idr_num ? 400 * rc->bpf / 100 : rc->bpf << 2;  /* iIdrBitrateRatio 400 % */
+    else {
+        const int rw = rc->remaining_weights, wt = rc->tl_weight;
+        int tb;
+        if (rw >= wt)  /* rw == wt divides too: bFixRCOverShoot */
+            tb = rw == 0 ? (int)(uint32_t)((uint64_t)(uint32_t)rc->remaining * (uint64_t)(uint32_t)wt)
+                         : (int)(((int64_t)(rw / 2) + (int64_t)rc->remaining * wt) / rw);
+        else tb = rc->remaining;
+        if (tb <= 0 && !rc->skip_en) rc->bits_level = 2;
+        rc->target = clip3(rc->min_bits_tl, rc->max_bits_tl, tb);
+    }
+    rc->remaining_weights -= rc->tl_weight;
+    if (idr) {  /* RcCalculateIdrQp (766790-767604) */
+        int cls, i;
+        rc_idr_class(w, h, rc->bitrate, &cls, &i);
+        const int lo = clip3(QP_MIN, QP_MAX, OH_RC_QP_RANGE[i][1]), hi = clip3(QP_MIN, QP_MAX, OH_RC_QP_RANGE[i][0]);
+        int q;
+        if (rc->idr_num == 0) q = OH_RC_INIT_QP[cls][i];
+        else {
+            if (rc->nmb != rc->intra_mb_count) rc->intra_cmplx = rc->intra_cmplx * rc->nmb / rc->intra_mb_count;
+            q = h264o_rc_qstep2qp(qstep_model(rc->intra_cmplx, cmplx_ratio(rc->frame_cmplx, rc->intra_cmplx_mean), rc->target));
+        }
+        q = clip3(lo, hi, q);
+        rc->init_qp = q; rc->global_qp = q; rc->last_qscale = q; rc->qstep = OH_RC_QSTEP[q];
+        rc->max_frame_qp = clip3(lo, hi, q + IDR_QP_WINDOW);
+        rc->min_frame_qp = clip3(lo, hi, q - IDR_QP_WINDOW);
+    } else {    /* RcCalculatePictureQp (767612-768334); one temporal layer: no temporal QP delta */
+        int q;
+        if (rc->pframe_num == 0) q = rc->init_qp;
+        else if (rc->bits_level == 2) q = rc->last_qscale + 3;
+        else {
+            rc->qstep = qstep_model(rc->linear_cmplx, cmplx_ratio(rc->frame_cmplx, rc->frame_cmplx_mean), rc->target);
+            q = h264o_rc_qstep2qp(rc->qstep);
+        }
+        rc->min_frame_qp = clip3(QP_MIN, QP_MAX, rc->last_qscale - FRAME_DQP_LOWER);
+        rc->max_frame_qp = clip3(QP_MIN, QP_MAX, rc->last_qscale + FRAME_DQP_UPPER);
+        q = clip3(rc->min_frame_qp, rc->max_frame_qp, q);
+        rc->last_qscale = q; rc->qstep = OH_RC_QSTEP[q]; rc->global_qp = q;
+    }
+    /* RcInitSliceInformation / RcInitGomParameters (768342-769173), the slice's RC init (func 225) */
+    rc->bits_per_mb = (int)(uint32_t)(uint64_t)(rc->nmb == 0 ? (int64_t)rc->target * 100
+                                                            : ((int64_t)(rc->nmb / 2) + (int64_t)rc->target * 100) / rc->nmb);
+    rc->avg_qp = 0;
+    rc->complexity_index = 0;
+    rc->calc_qp = rc->global_qp;
+    rc->total_qp = rc->total_mb = 0;
+    rc->frame_bits_slice = rc->gom_bits_slice = rc->gom_target_bits = 0;
+    rc->target_bits_slice = (int)(uint32_t)(uint64_t)(((int64_t)rc->nmb * rc->bits_per_mb + 50) / 100);
+}
+/* WelsRcMbInitGom (func 1215) in exact-GOM mode: at the first MB of every GOM after the first, RcCalculateGomQp
+ * moves the QP by the slice's bits so far against the GOM targets (+2 / +1 / -1 at bit ratios 0.8409 / 0.9439 /
+ * 1.06; its -2 branch is unreachable), clipped to the frame's window; then RcGomTargetBits shares the remaining
+ * bits over the GOMs left by their complexity. Returns the MB's QP. I slices (bEnableGomQp 0 in RC_BITRATE_MODE,
+ * 766730-766775): the frame QP. */
+static int rc_mb_init_gom(Rc *rc, int mb, int idr) {
+    if (idr) return rc->global_qp;
+    if (mb % rc->mb_per_gom == 0) {
+        if (mb != 0) {  /* iStartMbSlice 0 */
+            rc->complexity_index++;
+            int d = 2;
+            const int left = rc->target_bits_slice - rc->frame_bits_slice;
+            if (left > 0) {
+                const int64_t tleft = (int64_t)left + rc->gom_bits_slice - rc->gom_target_bits;
+                if (tleft > 0) {
+                    const uint64_t ratio = (uint64_t)((int64_t)left * 10000) / (uint64_t)(tleft + 1);
+                    if (ratio >= 8409) d = ratio < 9439 ? 1 : -(ratio > 10600);
+                }
+            }
+            rc->calc_qp = clip3(rc->min_frame_qp, rc->max_frame_qp, rc->calc_qp + d);
+            rc->gom_bits_slice = 0;
+        }
+        /* RcGomTargetBits (759693-760199) */
+        const int last = (rc->nmb - 1) / rc->mb_per_gom, k = rc->complexity_index;
+        int left = rc->target_bits_slice - rc->frame_bits_slice;
+        if (left <= 0) left = 0;
+        else if (last > k) {
+            int sum = 0;
+            for (int i = k + 1; i <= last; i++) sum += (int)rc->gom_sad[i];
+            if (sum == 0) left = (left + (last - k) / 2) / (last - k);
+            else left = (int)(uint32_t)(uint64_t)(((int64_t)(sum / 2) + (int64_t)(int32_t)rc->gom_sad[k + 1] * (int64_t)(uint32_t)left) / sum);
+        }
+        rc->gom_target_bits = left;
+    }
+    return rc->calc_qp;
+}
+/* WelsRcMbInfoUpdateGom (func 1206): the MB's bits (its mb_skip_run code included) and, when it has any, its QP */
+static void rc_mb_update(Rc *rc, int bits, int qp) {
+    rc->frame_bits_slice += bits;
+    rc->gom_bits_slice += bits;
+    if (bits > 0) { rc->total_qp += qp; rc->total_mb++; }
+}
+/* WelsRcPictureInfoUpdateGom (func 1218) after a coded frame: slice_bytes = the slice NAL (start code and
+ * emulation prevention included; the parameter sets are another layer). RcUpdatePictureQpBits, the R-Q model
+ * (RcUpdateFrameComplexity func 676 / RcUpdateIntraComplexity), the VGOP budget and RcVBufferCalculationSkip. */
+static void rc_picture_update(Rc *rc, int idr, int slice_bytes) {
+    const int bits = slice_bytes << 3;
+    const int avg = (!idr && rc->total_mb > 0) ? (rc->total_mb * 50 + rc->total_qp * 100) / (rc->total_mb * 100) : rc->global_qp;
+    rc->last_qscale = avg;
+    rc->avg_qp = avg;
+    rc->gop_bits_dq += bits;
+    if (!idr) {
+        const int q = OH_RC_QSTEP[avg];
+        if (rc->pframe_num == 0) {
+            rc->frame_cmplx_mean = (int64_t)(int32_t)(uint32_t)(uint64_t)rc->frame_cmplx;
+            rc->linear_cmplx = (int64_t)bits * q;
+        } else {
+            rc->frame_cmplx_mean = (rc->frame_cmplx * 20 + rc->frame_cmplx_mean * 80 + 50) / 100;
+            rc->linear_cmplx = (rc->linear_cmplx * 80 + (int64_t)q * bits * 20 + 50) / 100;
+        }
+        rc->pframe_num = (rc->pframe_num >= 254 ? 254 : rc->pframe_num) + 1;
+    } else {
+        const int64_t ic = (int64_t)OH_RC_QSTEP[avg] * bits;
+        if (rc->idr_num == 0) { rc->intra_cmplx_mean = rc->frame_cmplx; rc->intra_cmplx = ic; }
+        else {
+            rc->intra_cmplx = (ic * 20 + rc->intra_cmplx * 80 + 50) / 100;
+            rc->intra_cmplx_mean = (rc->frame_cmplx * 20 + rc->intra_cmplx_mean * 80 + 50) / 100;
+        }
+        rc->intra_mb_count = rc->nmb;
+        rc->idr_num = (rc->idr_num >= 254 ? 254 : rc->idr_num) + 1;
+    }
+    rc->remaining -= bits;
+    if (rc->skip_en) {  /* RcVBufferCalculationSkip (761104-761644) */
+        rc->fullness += bits - rc->bpf;
+        int64_t pred = 0;
+        if (rc->frame_coded_in_vgop <= 6)
+            for (int i = rc->frame_coded_in_vgop + 1; i < VGOP_SIZE; i++) pred += rc->min_bits_tl;
+        const double inc = ((double)(pred - rc->remaining) * 100.0) / (double)(rc->bpf << 3) + -5.0;
+        if ((rc->fullness > rc->buffer_size_skip && rc->avg_qp > rc->skip_qp) || inc > (double)RC_VARY) rc->skip_flag = 1;
+    }
+    rc->frame_coded_in_vgop++;
+}
+/* The preprocessing's frame complexity (AnalyzeSpatialPic -> CComplexityAnalysis::Process, func 910) over the
+ * coded-size luma picture, one value per GOM of mb_per_gom MBs (written to gom_sad), the frame's = their uint32
+ * sum. P (GOM_SAD, GomSampleSad func 909): the four 8x8 SADs (VAACalcSad) of every MB against the last coded
+ * frame's source. I (GOM_VAR, VAACalcSadVar): per GOM, uint32 square sum - (uint32 sum)^2 / (MBs of the GOM's
+ * first row x 256). */
+static int64_t rc_complexity(Rc *rc, const uint8_t *cur, const uint8_t *ref, int stride, int idr) {
+    const int mbw = rc->mbw, nmb = rc->nmb;
+    uint32_t frame = 0;
+    for (int j = 0; j < rc->gom_count; j++) {
+        const int start = j * rc->mb_per_gom, end = imin((j + 1) * rc->mb_per_gom, nmb);
+        uint32_t sad = 0, sum = 0, sq = 0;
+        for (int m = start; m < end; m++) {
+            const uint8_t *c = cur + (size_t)(m / mbw) * 16 * stride + (m % mbw) * 16;
+            const uint8_t *r = ref + (size_t)(m / mbw) * 16 * stride + (m % mbw) * 16;
+            for (int y = 0; y < 16; y++)
+                for (int x = 0; x < 16; x++) {
+                    const int a = c[y * stride + x], b = r[y * stride + x];
+                    sad += (uint32_t)(a > b ? a - b : b - a);
+                    sum += (uint32_t)a;
+                    sq += (uint32_t)(a * a);
+                }
+        }
+        const uint32_t first_row = (uint32_t)(imin((start / mbw + 1) * mbw, end) - start);
+        const uint32_t v = idr ? sq - (sum * sum) / (first_row << 8) : sad;
+        rc->gom_sad[j] = v;
+        frame += v;
+    }
+    return (int64_t)frame;
+}
+/* this project's MB-row QP plan for P frames: rows that cost more than the mean in the last coded
+ * frame are quantised more coarsely, cheaper rows more finely, inside the frame's window */
 int h264o_rc_row_delta(int64_t row_bits, int64_t mean) {
     if (mean <= 0) return 0;
     if (row_bits > 2 * mean) return 2;
@@ -146,6 +452,9 @@ int h264o_table(const char *name, double *out) {
     else if (!strcmp(name, "rc_init_qp")) { for (int i = 0; i < 20; i++) out[n++] = OH_RC_INIT_QP[i / 5][i % 5]; }
     else if (!strcmp(name, "rc_qp_range")) { for (int i = 0; i < 10; i++) out[n++] = OH_RC_QP_RANGE[i / 2][i % 2]; }
     else if (!strcmp(name, "rc_qstep")) { for (int i = 0; i < 52; i++) out[n++] = OH_RC_QSTEP[i]; }
+    else if (!strcmp(name, "logf_table")) { for (int i = 0; i < 32; i++) out[n++] = OH_LOGF_T[i / 2][i % 2]; }
+    else if (!strcmp(name, "logf_poly")) { for (int i = 0; i < 4; i++) out[n++] = OH_LOGF_P[i]; }
+    else if (!strcmp(name, "rc_tl_weight")) { for (int i = 0; i < 16; i++) out[n++] = OH_RC_TL_WEIGHT[i / 4][i % 4]; }
     else if (!strcmp(name, "level_limits")) { for (int i = 0; i < 17 * 6; i++) out[n++] = OH_LEVEL_LIMITS[i / 6][i % 6]; }
     else return -1;
     return n;
@@ -692,19 +1001,34 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
     e->mbs = (MBInfo *)calloc((size_t)e->mbw * e->mbh, sizeof(MBInfo));
     e->rowqp = (int *)calloc((size_t)e->mbh, sizeof(int));
     e->rowbits = (int64_t *)calloc((size_t)e->mbh, sizeof(int64_t));
+    e->prev_src = (uint8_t *)calloc((size_t)e->cw * e->ch, 1);
+    e->rc.gom_sad = (uint32_t *)calloc((size_t)e->mbw * e->mbh, sizeof(uint32_t));
+    rc_init(&e->rc, w, h, bitrate);  /* frame skipping on: the wrapper leaves bEnableFrameSkip at its default */
     e->first = 1;
-    e->skip_en = 1;  /* the wrapper leaves OpenH264's frame skipping on (bEnableFrameSkip default) */
-    e->init_qp = h264o_rc_idr_params(w, h, bitrate, &e->rmin, &e->rmax);
-    e->qp = e->init_qp;
     e->idr_pic_id = 0;
     return e;
 }
 void h264o_enc_destroy(H264OEnc *e) {
     if (!e) return;
     for (int p = 0; p < 3; p++) { free(e->src[p]); free(e->rec[p]); free(e->ref[p]); }
+    free(e->prev_src); free(e->rc.gom_sad);
     free(e->mbs); free(e->rowqp); free(e->rowbits); free(e);
 }
-void h264o_enc_set_frame_skip(H264OEnc *e, int enable) { if (e) e->skip_en = enable != 0; }
+/* bEnableFrameSkip (on by default, as the wrapper leaves it): off, no frame is skipped, the VBV check is not
+ * made, and an exhausted VGOP budget raises the QP instead (BITS_EXCEEDED) */
+void h264o_enc_set_frame_skip(H264OEnc *e, int enable) { if (e) e->rc.skip_en = enable != 0; }
+void h264o_enc_set_gom_exact(H264OEnc *e, int enable) { if (e) e->gom_exact = enable != 0; }
+/* the rate control's state after the last encode call, for tests: {skipped (1 if that call skipped the frame),
+ * global QP, average QP, target bits, remaining bits, buffer fullness (low 32 bits), continual skips,
+ * frame complexity (low 32 bits), min frame QP, max frame QP, bits per frame, P frames coded, IDRs coded,
+ * skip flag, remaining weights, frames coded in the VGOP} */
+void h264o_enc_rc_state(const H264OEnc *e, int32_t out[16]) {
+    const Rc *r = &e->rc;
+    out[0] = e->last_skipped; out[1] = r->global_qp; out[2] = r->avg_qp; out[3] = r->target; out[4] = r->remaining;
+    out[5] = (int32_t)r->fullness; out[6] = r->continual_skip; out[7] = (int32_t)r->frame_cmplx; out[8] = r->min_frame_qp;
+    out[9] = r->max_frame_qp; out[10] = r->bpf; out[11] = r->pframe_num; out[12] = r->idr_num; out[13] = r->skip_flag;
+    out[14] = r->remaining_weights; out[15] = r->frame_coded_in_vgop;
+}
 int h264o_enc_frames_skipped(const H264OEnc *e) { return e ? e->skipped : 0; }
 void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]) {
     out[0] = e->stat_cross; out[1] = e->stat_cross_moved; out[2] = e->stat_nb_start;
@@ -729,12 +1053,14 @@ static void load_source(H264OEnc *e, const uint8_t *yuv) {
 int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     if (!e || !yuv || !out) return 0;
     int idr = e->first || e->force_idr;
-    const int64_t T = e->bitrate / RC_FPS;
-    /* frame skip: a non-IDR frame is dropped while the virtual buffer holds more
-     * than half a second of bits; nothing else changes (reference, frame_num, POC, QP plan) */
-    if (!idr && e->skip_en && e->vbuf > e->bitrate / 2) {
-        e->vbuf = e->vbuf > T ? e->vbuf - T : 0;
+    Rc *rc = &e->rc;
+    /* frame skip (func 589 / 1258 / 1254): a skipped frame leaves the reference, frame_num and
+     * the preprocessing's reference picture as they are; an IDR is never skipped */
+    e->last_skipped = 0;
+    if (rc_judge_skip(rc) && !idr) {
+        rc_post_skip(rc);
         e->skipped++;
+        e->last_skipped = 1;
         return 0;
     }
     load_source(e, yuv);
@@ -742,7 +1068,9 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     /* uiIdrPicId (a uint16) is incremented before the IDR's parameter sets are written (func 589, file
      * offset 378895), so the first IDR carries 1 when the counter starts at 0 */
     if (idr) { e->frame_num = 0; e->poc = 0; e->idr_pic_id = (e->idr_pic_id + 1) & 0xffff; }
-    int qp = rc_frame_qp(e, idr);
+    rc->frame_cmplx = rc_complexity(rc, e->src[0], e->prev_src, e->cw, idr);
+    rc_picture_init(rc, idr, e->w, e->h);
+    const int qp = rc->global_qp;
     size_t o = 0;
     uint8_t *tmp = (uint8_t *)malloc(64 + (size_t)e->cw * e->ch * 4);
     if (idr) { o += h264o_write_sps(e->w, e->h, e->bitrate, tmp + o); o += h264o_write_pps(tmp + o); }
@@ -773,10 +1101,13 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
      * QPY is the running QP (7.4.5) */
     int skip_run = 0, running = qp;
     for (int mby = 0; mby < e->mbh; mby++) {
-        const int qrow = clip3(e->qmin, e->qmax, qp + e->rowqp[mby]);
+        /* this project's row plan: P rows at the frame QP + the row's offset inside the frame's window; an IDR
+         * is coded at the frame QP (OpenH264 turns the GOM QP off for I slices in RC_BITRATE_MODE) */
+        const int qplan = idr ? qp : clip3(rc->min_frame_qp, rc->max_frame_qp, qp + e->rowqp[mby]);
         e->rowbits[mby] = 0;
         for (int mbx = 0; mbx < e->mbw; mbx++) {
             MBInfo *mb = &e->mbs[mby * e->mbw + mbx];
+            const int qrow = e->gom_exact ? rc_mb_init_gom(rc, mby * e->mbw + mbx, idr) : qplan;
             memset(mb, 0, sizeof(*mb));
             mb->qp = qrow;
             for (int i = 0; i < 16; i++) mb->i4mode[i] = 2;
@@ -787,25 +1118,29 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
             const int dqp = carries ? qp_delta_wrap(qrow, running) : 0;
             if (carries) running = qrow;
             mb->qp = running;
-            if (mb->type == MBT_PSKIP) { skip_run++; continue; }
+            if (mb->type == MBT_PSKIP) { skip_run++; rc_mb_update(rc, 0, running); continue; }
+            const int64_t bs = bw_bits(&b);
             if (!idr) { bw_ue(&b, (uint32_t)skip_run); skip_run = 0; }
             const int64_t b0 = bw_bits(&b);
             write_mb(&b, e, mb, mbx, mby, !idr, dqp);
             e->rowbits[mby] += bw_bits(&b) - b0;
+            rc_mb_update(rc, (int)(bw_bits(&b) - bs), running);
         }
     }
     if (skip_run) bw_ue(&b, (uint32_t)skip_run);
     bw_trailing(&b);
+    const size_t o_slice = o;
     o += nal_write(tmp + o, 3, idr ? 5 : 1, b.buf, b.len);
     bw_free(&b);
     /* loop filter on the reconstruction -> next reference */
     deblock_frame(e->rec[0], e->rec[1], e->rec[2], e->cw, e->cw / 2, e->mbs, e->mbw, e->mbh, 0);
     for (int p = 0; p < 3; p++) { uint8_t *t = e->ref[p]; e->ref[p] = e->rec[p]; e->rec[p] = t; }
     e->last_qp = qp; e->last_idr = idr;
-    e->last_bits = (int64_t)o * 8;
-    e->vbuf = e->vbuf + e->last_bits > T ? e->vbuf + e->last_bits - T : 0;
-    e->qp = h264o_rc_next_qp(qp, e->last_bits, e->bitrate, idr);
+    /* the RC update on the slice NAL's size (func 1218: iLayerSize of the slice layer, 677356 / 683472) */
+    rc_picture_update(rc, idr, (int)(o - o_slice));
     rc_plan_rows(e);
+    /* the preprocessing's reference picture is the last coded frame's source (UpdateSrcList) */
+    memcpy(e->prev_src, e->src[0], (size_t)e->cw * e->ch);
     e->frame_num = (e->frame_num + 1) & ((1 << LOG2_MAX_FRAME_NUM) - 1);
     e->poc += 2;
     int n = (int)o;

@@ -20,7 +20,11 @@ class Oracle:
         L.h264o_enc_frames_skipped.argtypes = [vp]
         L.h264o_enc_me_stats.argtypes = [vp, vp]
         L.h264o_rc_init_qp.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
-        L.h264o_rc_next_qp.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+        L.h264o_rc_qstep2qp.argtypes = [ctypes.c_int32]
+        L.h264o_logf.argtypes = [ctypes.c_float]
+        L.h264o_logf.restype = ctypes.c_float
+        L.h264o_enc_set_gom_exact.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.h264o_enc_rc_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.h264o_write_sps.restype = ctypes.c_size_t
         L.h264o_write_sps.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
         L.h264o_write_pps.restype = ctypes.c_size_t
@@ -70,6 +74,18 @@ class OEnc:
 
     def set_frame_skip(self, on):
         self.L.h264o_enc_set_frame_skip(self.e, 1 if on else 0)
+
+    def set_gom_exact(self, on):
+        self.L.h264o_enc_set_gom_exact(self.e, 1 if on else 0)
+
+    RC_FIELDS = ('skipped', 'qp', 'avg_qp', 'target', 'remaining', 'fullness', 'continual', 'cmplx', 'min_qp',
+                 'max_qp', 'bpf', 'pframes', 'idrs', 'skip_flag', 'remaining_weights', 'coded_in_vgop')
+
+    def rc_state(self):
+        """the rate control's state after the last encode call (oracle h264o_enc_rc_state)"""
+        out = (ctypes.c_int32 * 16)()
+        self.L.h264o_enc_rc_state(self.e, out)
+        return dict(zip(self.RC_FIELDS, list(out)))
 
     def recon(self):
         out = np.zeros(self.w * self.h * 3 // 2, np.uint8)

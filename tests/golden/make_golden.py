@@ -102,6 +102,7 @@ def main():
     # one small Annex-B stream kept verbatim for decoder regression tests (I + P frames)
     frames, _ = case_inputs(oracle, 176, 144, 3, 'synth', seed=3)
     enc = oracle.encoder(176, 144, 200000)
+    enc.set_frame_skip(False)  # three coded pictures (the rate control would skip the P frames at this bitrate)
     stream = b''.join(enc.encode(f) for f in frames)
     with open(os.path.join(HERE, 'synth3_qcif_3f.h264'), 'wb') as f:
         f.write(stream)

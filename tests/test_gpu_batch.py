@@ -79,6 +79,8 @@ def test_module_facade_replays_worker_sequence(gpu_lib, oracle):
         off, n = M.getValue(outpp, 'i32'), M.getValue(outsz, 'i32')
         nal = bytes(M.HEAPU8[off:off + n])
         assert nal == oe.encode(f)
+        if n == 0:  # skipped by the rate control (the worker posts no frame, encoder_worker.js:167)
+            continue
         M.HEAPU8[nalp:nalp + n] = nal
         decode(1, nalp, n, dst, wp, hp)
         assert (M.getValue(wp), M.getValue(hp)) == (w, h)

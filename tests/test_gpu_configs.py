@@ -70,12 +70,45 @@ def test_config3_1080p_ippp_8mbps_60_frames(gpu_lib, oracle):
 
 
 def test_config3_1080p_ippp_1mbps_rc_skipping(gpu_lib, oracle):
-    """configs[2] at the glue's 1 Mbps with the wrapper's frame skipping: the rate control drops the
-    frames its buffer cannot take (0-byte access units) -- GPU == oracle, including which
-    frames are skipped; every coded frame decodes to the oracle's picture"""
-    sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 1000000, 12, False)
-    assert sizes[0] > 0 and 0 in sizes[1:], sizes
+    """configs[2] at its 60-frame span and the glue's 1 Mbps with the wrapper's frame skipping (OpenH264's
+    RC_BITRATE_MODE restated from h264.wasm): the IDR overfills the skip buffer, frames are
+    skipped (0-byte access units) until the cap on the run of skipped frames -- (round(fullness / bits per frame)
+    + 1) >> 1 >= the run, CheckFrameSkipBasedMaxbr -- forces a P frame through at frame 40. GPU == oracle frame
+    by frame, the skips and the forced P frame included; every coded frame decodes to the oracle's picture."""
+    sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 1000000, 60, False)
     assert qps[0] == 36, qps  # RcCalculateIdrQp at 1 Mbps, 60 fps default: bpp 0.008 -> QP 36 in [28, 40]
+    assert sizes[0] > 0 and all(n == 0 for n in sizes[1:40]) and sizes[40] > 0, sizes
+    assert qps[40] == 36  # the first P frame takes the IDR's QP (RcCalculatePictureQp, iPFrameNum 0)
+
+
+def test_rc_state_batch_vs_oracle(gpu_lib, oracle):
+    """the device rate control's whole state (skip decision, QP and window, target and remaining bits, buffer
+    fullness, run of skips, frame complexity, VGOP counters) == the oracle's after every frame, 1080p, two
+    streams at 8 Mbps with skipping on (coded / skipped alternation after the IDR's overspend) and a forced
+    IDR at frame 9 (the intra R-Q model's QP)"""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    w, h, br, S, nf = 1920, 1080, 8000000, 2, 14
+    gs = [SyntheticStream(s, w, h) for s in range(S)]
+    enc = h264mi.BatchEncoder(w, h, br, S)
+    oes = [oracle.encoder(w, h, br) for _ in range(S)]
+    coded = 0
+    for t in range(nf):
+        fr = [np.ascontiguousarray(g.frame(t)) for g in gs]
+        if t == 9:
+            enc.force_idr()
+            for oe in oes:
+                oe.force_idr()
+        enc.encode(torch.from_numpy(np.stack(fr)).cuda())
+        n = enc.nal_sizes()
+        for s in range(S):
+            ref = oes[s].encode(fr[s])
+            assert n[s] == len(ref) and (n[s] == 0 or enc.nal_bytes(s, n[s]) == ref), f'frame {t} stream {s}'
+            assert enc.rc_state(s) == oes[s].rc_state(), f'frame {t} stream {s}'
+            coded += n[s] > 0
+    assert 2 * S <= coded < S * nf  # both coded and skipped frames were exercised
+    enc.close()
 
 
 @pytest.mark.parametrize('br', [1000000, 8000000], ids=['1mbps', '8mbps'])

@@ -52,6 +52,7 @@ def test_decoder_rgba_matches_oracle(gpu_lib, oracle):
     L = gpu_lib
     g = SyntheticStream(9, w, h)
     oe, od = oracle.encoder(w, h, 1500000), oracle.decoder()
+    oe.set_frame_skip(False)  # every frame coded
     assert L.init_decoder(5) == 0
     for t in range(4):
         nal = oe.encode(np.ascontiguousarray(g.frame(t)))
@@ -132,6 +133,7 @@ def test_decoder_frame_copy_concealment(gpu_lib, oracle):
     L = gpu_lib
     assert L.init_decoder(9) == 0
     oe, od = oracle.encoder(w, h, 300000), oracle.decoder()
+    oe.set_frame_skip(False)  # every frame coded
     g = SyntheticStream(4, w, h)
     units = [oe.encode(np.ascontiguousarray(g.frame(t))) for t in range(6)]
     units[2] = units[2][:len(units[2]) // 2]                                        # truncated slice

@@ -71,6 +71,7 @@ def test_ring_drop_semantics_match_js_pool(gpu_lib):
     import h264mi
     w, h = 176, 144
     enc = h264mi.BatchEncoder(w, h, 300000, 1)
+    enc.set_frame_skip(False)  # the ring semantics under test need a unit per frame
     frames = _frames(w, h, 8, 3)
     ring = h264mi.NalRing(slots=2, slot_bytes=1 << 16)
     model = JsPool(2, 1 << 16)
@@ -141,10 +142,12 @@ def test_ring_fanout_zero_copy_decoders(gpu_lib, oracle):
     es = torch.cuda.Stream()
     dss = [torch.cuda.Stream() for _ in range(D)]
     enc = h264mi.BatchEncoder(w, h, 1000000, 1, stream=es)
+    enc.set_frame_skip(False)  # every frame coded and published
     decs = [h264mi.BatchDecoder(w, h, 1, stream=dss[k]) for k in range(D)]
     ring = h264mi.NalRing(slots=4, slot_bytes=1 << 20)
     od = oracle.decoder()
     oe = oracle.encoder(w, h, 1000000)
+    oe.set_frame_skip(False)
     for t in range(n):
         with torch.cuda.stream(es):
             es.wait_stream(torch.cuda.current_stream())
@@ -186,6 +189,7 @@ def test_ring_wraps_without_host_sync(gpu_lib):
     es = torch.cuda.Stream()
     dss = [torch.cuda.Stream() for _ in range(D)]
     enc = h264mi.BatchEncoder(w, h, 300000, 1, stream=es)
+    enc.set_frame_skip(False)  # the ring semantics under test need a unit per frame
     decs = [h264mi.BatchDecoder(w, h, 1, stream=dss[k]) for k in range(D)]
     ring = h264mi.NalRing(slots=2, slot_bytes=1 << 18)
     torch.cuda.synchronize()
@@ -224,6 +228,7 @@ def test_ring_failed_frame_publishes_nothing(gpu_lib, oracle, code):
     w, h, n, bad = 176, 144, 5, 2
     frames = _frames(w, h, n, 7)
     enc = h264mi.BatchEncoder(w, h, 300000, 1)
+    enc.set_frame_skip(False)  # the ring semantics under test need a unit per frame
     enc.set_frame_skip(False)
     dec = h264mi.BatchDecoder(w, h, 1)
     ring = h264mi.NalRing(slots=4, slot_bytes=1 << 18)

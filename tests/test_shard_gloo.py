@@ -96,7 +96,8 @@ def _group_worker(rank, world, port, q):
             for j in range(n):
                 for i, sid in enumerate(stream_ids(rank, S)):
                     u = units[sid][t + j]
-                    stage[b][j, i * slot:i * slot + len(u)] = torch.frombuffer(bytearray(u), dtype=torch.uint8)
+                    if u:  # a frame the rate control skipped is an empty unit
+                        stage[b][j, i * slot:i * slot + len(u)] = torch.frombuffer(bytearray(u), dtype=torch.uint8)
                     stage_sz[b][j, i] = len(u)
             gat.submit(stage[b], stage_sz[b], n, b)
             if rank == 0 and len(gat.received) > len(got):

@@ -5,7 +5,7 @@ Test infrastructure / study aid. It decodes the module's sections and every func
 C-like listing so that OpenH264's encoder logic can be READ: which constants its parameter-set writers
 put into the stream, which rules its rate control applies. Nothing is instantiated, interpreted,
 translated into something runnable or linked; the listing is text for a human and for
-`tools/wasm_syntax.py`, which cites the file offsets it finds.
+`tools/wasm_tables.py`, which cites the file offsets it finds.
 
 Listing conventions: `L3` = local 3 (parameters first), `G0` = global 0, `t17` = the result of a call,
 `u8[x+4]` / `i32[x+12]` = loads (signed: `s8`, `s16`), stores are `i32[x+12] = v`; every statement carries
@@ -295,13 +295,15 @@ class Dis:
                 l, i = uleb(b, i)
                 tgt = len(ctl) - 1 - l
                 kw = ctl[tgt][0] if tgt >= 0 else 'func'
-                self.emit(depth, f'br B{tgt} ({kw}{"=continue" if kw == "loop" else ""})', off)
+                carry = f' carry {stack[-1]}' if tgt >= 0 and kw != 'loop' and ctl[tgt][2] and stack else ''
+                self.emit(depth, f'br B{tgt} ({kw}{"=continue" if kw == "loop" else ""}){carry}', off)
             elif op == 0x0d:
                 l, i = uleb(b, i)
                 c = pop()
                 tgt = len(ctl) - 1 - l
                 kw = ctl[tgt][0] if tgt >= 0 else 'func'
-                self.emit(depth, f'br_if ({c}) B{tgt} ({kw}{"=continue" if kw == "loop" else ""})', off)
+                carry = f' carry {stack[-1]}' if tgt >= 0 and kw != 'loop' and ctl[tgt][2] and stack else ''
+                self.emit(depth, f'br_if ({c}) B{tgt} ({kw}{"=continue" if kw == "loop" else ""}){carry}', off)
             elif op == 0x0e:
                 n, i = uleb(b, i)
                 ls = []

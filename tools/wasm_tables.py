@@ -154,6 +154,10 @@ TABLES = {
     'rc_init_qp': (43568, 'i', (4, 5), 'RcCalculateIdrQp initial IDR QP [iBppIndex][i]'),
     'rc_qp_range': (43648, 'i', (5, 2), 'RcCalculateIdrQp {max, min} QP of the IDR [i]'),
     'rc_qstep': (43696, 'i', (52,), 'g_kiQpToQstepTable (RcConvertQp2QStep): round(100 * 2^((qp - 4) / 6))'),
+    'rc_tl_weight': (43376, 'i', (4, 4), 'g_kiTlWeight[iDecompositionStages][temporal id] (RcInitTlWeight, func 702): '
+                     'one temporal layer -> row 0, weight 2000 = WEIGHT_MULTIPLY'),
+    'logf_table': (73408, 'd', (16, 2), 'musl logf {invc, logc}[16] (func 483, called by RcConvertQStep2Qp in func 1226)'),
+    'logf_poly': (73664, 'd', (4,), 'musl logf {Ln2, A[0], A[1], A[2]} (func 483)'),
     'level_limits': (63120, 'i', (17, 8), 'g_ksLevelLimits {level_idc, MaxMBPS, MaxFS, MaxDpbMbs, MaxBR, MaxCPB, MinVmv, MaxVmv} '
                      '(WelsInitSps, func 280, walks it in this order)'),
 }
@@ -177,6 +181,36 @@ CODE_CONSTANTS = {
     'area_90p': (766979, 'i32.const', 1226, 'iBppIndex 0 when w * h < this (<= 28800)'),
     'area_180p': (766991, 'i32.const', 1226, 'iBppIndex 1 when w * h < this'),
     'area_360p': (767005, 'i32.const', 1226, 'iBppIndex 2 when w * h < this, else 3'),
+    # frame-level rate control (oracle rc_* in h264o_enc.c; GPU enc_bits.inc)
+    'rc_vary_percentage': (689577, 'i32.const', 1021, 'InitializeExt: iRcVaryPercentage default (RcInitSequenceParameter '
+                           'copies it to iRcVaryPercentage / iRcVaryRatio)'),
+    'skip_qp_value_narrow': (401275, 'i32.const', 592, 'iSkipQpValue when the picture is < 31 MBs wide'),
+    'skip_qp_value_wide': (401277, 'i32.const', 592, 'iSkipQpValue otherwise (VBV skip needs the average QP above it)'),
+    'gom_rows_narrow': (401339, 'i32.const', 592, 'iNumberMbGom = mbw * (this + ...) below 31 MBs wide'),
+    'gom_rows_wide': (401341, 'i32.const', 592, 'iNumberMbGom = mbw * (this + (4 - 2) * vary / 100) from 31 MBs wide'),
+    'vgop_gops': (462240, 'i32.const', 702, 'RcInitTlWeight: iGopNumberInVGop = this >> iDecompositionStages (VGOP_SIZE)'),
+    'vgop_bits_shift': (764394, 'i32.const', 1226, 'RcInitVGop: iRemainingBits += iBitsPerFrame << this (VGOP_SIZE 8)'),
+    'weight_multiply': (764433, 'i32.const', 1226, 'RcInitVGop: iRemainingWeights = iGopNumberInVGop * this'),
+    'min_bits_base': (458364, 'i32.const', 697, 'RcUpdateBitrateFps: iMinBitsTl ratio = this - ((this - vary) >> 1)'),
+    'max_bits_ratio': (458356, 'i64.const', 697, 'RcUpdateBitrateFps: iMaxBitsTl ratio (percent)'),
+    'bits_tl_divisor': (458411, 'i64.const', 697, 'RcUpdateBitrateFps: divisor of gop bits x ratio x weight (100 x 2000)'),
+    'first_idr_target_shift': (766523, 'i32.const', 1226, 'RcDecideTargetBits: the first IDR targets iBitsPerFrame << this'),
+    'continual_skip_reset': (763777, 'i32.const', 1226, 'WelsRcPictureInitGom: iContinualSkipFrames = this on every coded frame'),
+    'qstep_min': (767923, 'i32.const', 1226, 'RcConvertQStep2Qp: QP 0 below this QStep'),
+    'qstep_conv_ln2': (767435, 'f64.const', 1226, 'RcConvertQStep2Qp: / this (ln 2) after 6 * logf(QStep / 100)'),
+    'qstep_conv_offset': (767445, 'f64.const', 1226, 'RcConvertQStep2Qp: + this'),
+    'qstep_conv_round': (767455, 'f64.const', 1226, 'RcConvertQStep2Qp: + this, then truncation'),
+    'cmplx_decay_new': (450973, 'i64.const', 676, 'RcUpdateFrameComplexity: weight of the new frame (of 100)'),
+    'cmplx_decay_old': (450981, 'i64.const', 676, 'RcUpdateFrameComplexity: weight of the running mean / model'),
+    'intra_decay_new': (760958, 'i64.const', 1218, 'RcUpdateIntraComplexity: weight of the new IDR'),
+    'vbv_percent': (761473, 'f64.const', 1218, 'RcVBufferCalculationSkip: dIncPercent scale'),
+    'vbv_percent_diff': (761493, 'f64.const', 1218, 'RcVBufferCalculationSkip: + this (-VGOP_BITS_PERCENTAGE_DIFF)'),
+    'vbv_vgop_shift': (761488, 'i32.const', 1218, 'RcVBufferCalculationSkip: divisor iBitsPerFrame << this'),
+    'gom_ratio_scale': (759582, 'i64.const', 1215, 'RcCalculateGomQp: iBitsRatio = this * left bits / (target left + 1)'),
+    'gom_ratio_up2': (759595, 'i64.const', 1215, 'RcCalculateGomQp: QP + 2 below this ratio'),
+    'gom_ratio_up1': (759608, 'i64.const', 1215, 'RcCalculateGomQp: QP + 1 below this ratio'),
+    'gom_ratio_down1': (759623, 'i64.const', 1215, 'RcCalculateGomQp: QP - 1 above this ratio'),
+    'gom_var_sample_shift': (530814, 'i32.const', 910, 'AnalyzeGomComplexityViaVar: sample count = first-row MBs << this'),
     # stream syntax (oracle h264o_write_sps / h264o_enc_encode)
     'sps_log2_max_frame_num_and_poc_type': (167923, 'i64.const', 280, 'WelsInitSps: one i64 store of '
                                             '{uiLog2MaxFrameNum (low word), uiPocType (high word)}'),
@@ -208,6 +242,9 @@ def decode_const(b, off, op):
     if op == 'i64.const':
         assert b[off] == 0x42, f'no i64.const at {off}'
         return sleb(b, off + 1)[0]
+    if op == 'f64.const':
+        assert b[off] == 0x44, f'no f64.const at {off}'
+        return struct.unpack_from('<d', b, off + 1)[0]
     raise ValueError(op)
 
 
