@@ -149,7 +149,9 @@ int h264mi_dec_streamed(h264mi_decoder *d);
    device uint32 *d_counter has reached target + f * step (wrap-safe comparison), or after limit_us microseconds
    of waiting -- a scheduling hint, never a correctness condition. With an encoder's rows counter
    (h264mi_enc_rows_counter) it starts each reconstruction in the tail of a concurrent encoder launch instead of
-   beside its densest part. count 0 clears it. Returns 0, -1 on a bad argument. */
+   beside its densest part. count 0 clears it. The gate is consumed by the next call whether that call succeeds or
+   fails; the memory behind d_counter (an encoder's rows counter) must outlive that call's reconstruction (destroy
+   the encoder only after synchronising the decoder). Returns 0, -1 on a bad argument. */
 int h264mi_dec_set_recon_gate(h264mi_decoder *d, const uint32_t *d_counter, uint32_t target, uint32_t step, int count, int limit_us);
 /* automatic streaming's process-wide budget in reconstruction waves (default: a quarter of dec_recon_kernel's
    resident wave slots on the current device, from its CU count and occupancy); waves <= 0 restores the

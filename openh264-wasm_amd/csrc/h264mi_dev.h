@@ -307,12 +307,17 @@ template <class P> DEV void gran_store2(P base, int idx, uint32_t epoch, uint32_
 #ifndef H264MI_WAIT_LIMIT_MS
 #define H264MI_WAIT_LIMIT_MS 2000
 #endif
+// The budget is a device global (ticks of the 100 MHz clock): the host sets it from the environment variable
+// H264MI_WAIT_LIMIT_MS when an encoder or decoder is created (wait_limit_from_env), e.g. for a GPU shared with
+// other processes. One WaitClock bounds one whole wait: gran_wait / the deblocking rows' get() pass theirs to
+// gran_wait1, so a wait over a set of granules is bounded by one budget, not one per stale granule.
+__device__ uint64_t g_wait_limit_ticks = (uint64_t)H264MI_WAIT_LIMIT_MS * 100000u;
 struct WaitClock {
     uint64_t t0 = 0;
     DEV bool expired() {
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         if (t0 == 0) { t0 = t; return false; }
-        return t - t0 > (uint64_t)H264MI_WAIT_LIMIT_MS * 100000u;
+        return t - t0 > __hip_atomic_load(&g_wait_limit_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 };
 
@@ -323,8 +328,7 @@ struct WaitClock {
 #ifndef H264MI_GRAN_WAIT1
 #define H264MI_GRAN_WAIT1 1
 #endif
-template <class P> DEV bool gran_wait1(P g, uint32_t epoch, int32_t *abort_word, unsigned &spins) {
-    WaitClock wc;
+template <class P> DEV bool gran_wait1(P g, uint32_t epoch, int32_t *abort_word, unsigned &spins, WaitClock &wc) {
     for (;; spins++) {
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -344,9 +348,7 @@ template <class P> DEV bool gran_wait1(P g, uint32_t epoch, int32_t *abort_word,
 template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, int32_t *abort_word) {
     int lane = threadIdx.x & 63;
     uint32_t val = 0;
-#if !H264MI_GRAN_WAIT1
     WaitClock wc;
-#endif
     for (unsigned spins = 0;; spins++) {
         bool ok = true;
         if (lane < n) {
@@ -357,7 +359,7 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
         const uint64_t bad = __ballot(!ok);
         if (bad == 0) break;
 #if H264MI_GRAN_WAIT1
-        if (!gran_wait1(g + (int)__builtin_ctzll(bad), epoch, abort_word, spins)) return false;
+        if (!gran_wait1(g + (int)__builtin_ctzll(bad), epoch, abort_word, spins, wc)) return false;
 #else
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -76,7 +76,7 @@ def _oracle_units(sid, nf, w=176, h=144):
     return [e.encode(np.ascontiguousarray(g.frame(t))) for t in range(nf)]
 
 
-def _group_worker(rank, world, port, q):
+def _group_worker(rank, world, port, q, S=2, G=3, nframes=7, w=176, h=144):
     import sys
     sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -84,8 +84,8 @@ def _group_worker(rank, world, port, q):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         from h264mi.shard import NalGather, stream_ids
-        S, G, slot, NB, nframes = 2, 3, 1 << 16, 3, 7  # groups of 3, 3, 1 frames
-        units = {sid: _oracle_units(sid, nframes) for sid in stream_ids(rank, S)}
+        slot, NB = 1 << 17, 3  # default: groups of 3, 3, 1 frames
+        units = {sid: _oracle_units(sid, nframes, w, h) for sid in stream_ids(rank, S)}
         gat = NalGather(dist, torch, S, slot, G, rank, world, None)
         stage = [torch.zeros((G, S * slot), dtype=torch.uint8) for _ in range(NB)]
         stage_sz = [torch.zeros((G, S), dtype=torch.int32) for _ in range(NB)]
@@ -107,8 +107,8 @@ def _group_worker(rank, world, port, q):
         gat.flush()
         if rank == 0:
             got.append(_snapshot(gat, world, S, slot, gat.received[-1], len(gat.received[-1]) // (world * S)))
-            everything = {sid: _oracle_units(sid, nframes) for sid in range(world * S)}
-            ok, t0 = len(got) == 3, 0
+            everything = {sid: _oracle_units(sid, nframes, w, h) for sid in range(world * S)}
+            ok, t0 = len(got) == (nframes + G - 1) // G, 0
             for grp in got:
                 n = len(grp) // (world * S)
                 for r in range(world):
@@ -117,7 +117,7 @@ def _group_worker(rank, world, port, q):
                             ok = ok and grp[(r * n + j) * S + i] == everything[r * S + i][t0 + j]
                 t0 += n
             # one packed message per sending rank and group, not one per access unit
-            q.put(bool(ok and t0 == nframes and gat.messages == 3 * (world - 1)))
+            q.put(bool(ok and t0 == nframes and gat.messages == len(got) * (world - 1)))
     finally:
         dist.destroy_process_group()
 
@@ -138,6 +138,24 @@ def test_group_gather_real_units(world):
         p.start()
     for p in procs:
         p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
+
+
+def test_config5_topology_world8():
+    """BASELINE configs[4]'s exact topology on gloo: 8 ranks x 4 streams (32 streams), groups of 4 frames as
+    bench.py stages them, real oracle access units (352x288 at the wrapper's default frame skipping: ragged
+    sizes and empty units), ONE packed message per sending rank and group; rank 0 checks every unit of all 32
+    streams byte for byte. (Unmeasured on hardware until the driver's SCALE run: this is its data path.)"""
+    world = 8
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, world, port, q, 4, 4, 6, 352, 288)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
 
