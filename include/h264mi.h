@@ -86,6 +86,10 @@ int h264mi_enc_encode(h264mi_encoder *e, const void *d_frames);     /* async; ns
 /* rate-control frame skipping (on by default, as the wrapper's OpenH264): a skipped frame has 0 NAL bytes */
 int h264mi_enc_set_frame_skip(h264mi_encoder *e, int enable);
 int h264mi_enc_frames_skipped(h264mi_encoder *e, int stream);
+/* OpenH264's GOM rate control exactly (WelsRcMbInitGom / WelsRcMbInfoUpdateGom): a P frame's GOM (2 MB rows from
+   31 MBs wide) takes its QP from the bits of every MB before it, so a stream keeps one GOM in flight; off (the
+   default unless H264MI_GOM_EXACT=1 at creation): this project's MB-row QP plan inside the frame's window */
+int h264mi_enc_set_gom_exact(h264mi_encoder *e, int enable);
 /* test hook: the next coded frame of stream fails as if its kernels had reported error code (> 0): it
    publishes 0 NAL bytes and the frame after it is an IDR. Code 3 fails it through enc_pack_kernel's
    RBSP-overflow branch itself (the early exit before the slice is assembled) */
@@ -102,6 +106,10 @@ int h264mi_enc_last_qp(h264mi_encoder *e, int stream);
    buffer fullness, continual skips, frame complexity, min / max frame QP, bits per frame, P frames, IDRs,
    skip flag, remaining weights, frames coded in the VGOP} */
 int h264mi_enc_rc_state(h264mi_encoder *e, int stream, int *out16);
+/* exact GOM mode, the last coded P frame: per GOM {QP, slice bits before it, target bits, last coded MB + 1}
+   (4 int32 each, up to cap values; the oracle's h264o_enc_gom_state). Returns the GOM count (out NULL or the
+   mode off: nothing copied) */
+int h264mi_enc_gom_state(h264mi_encoder *e, int stream, int *out, int cap);
 /* RcConvertQStep2Qp as the device computes it (thresholds; the wasm's musl-logf form is the oracle's) */
 int h264mi_rc_qstep_to_qp(int qstep);
 int h264mi_enc_mbinfo(h264mi_encoder *e, int stream, void *host_out); /* 128 B per MB (h264mi_types.h MbInfo) */

@@ -69,7 +69,7 @@ struct RcState {
     int32_t init_qp, last_qscale, qstep, avg_qp, min_frame_qp, max_frame_qp;  // rc+8, +224, +212, +144, +148, +152
     int32_t idr_num, intra_mb_count, pframe_num;  // rc+76, rc+88, tl+24
     int32_t prev_idx;                         // which psrc holds the last coded frame's luma
-    int32_t pad0;
+    int32_t target_bits_slice;                // sl+1372 iTargetBitsSlice (exact GOM mode)
     int64_t fullness;                         // rc+232
     int64_t intra_cmplx, intra_cmplx_mean;    // rc+80, rc+96
     int64_t linear_cmplx, frame_cmplx_mean;   // tl+16, tl+32
@@ -125,6 +125,8 @@ struct EncDesc {
     uint8_t *psrc[2];       // coded-size luma of the last coded frame and of the frame being coded (RcState::prev_idx):
                             // the preprocessing's reference picture for the frame complexity (enc_cmplx_kernel)
     uint32_t *gomc;         // per GOM: [0, G) SAD against the last coded source (P), [G, 2G) variance (I)
+    uint64_t *bitg;         // exact GOM mode: per MB {epoch, macroblock_layer() bits} granules (the CAVLC waves)
+    uint64_t *gomst;        // exact GOM mode: per GOM 4 granules {QP, slice bits before it, target bits, last coded MB + 1}
 };
 
 // One stream's padded reference planes and the picture they are built from (enc_planes.inc).

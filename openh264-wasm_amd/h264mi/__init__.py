@@ -47,6 +47,7 @@ def lib():
             'h264mi_enc_encode': (i, [vp, vp]),
             'h264mi_enc_set_frame_skip': (i, [vp, i]),
             'h264mi_enc_frames_skipped': (i, [vp, i]),
+            'h264mi_enc_set_gom_exact': (i, [vp, i]),
             'h264mi_enc_inject_error': (i, [vp, i, i]),
             'h264mi_enc_sync': (i, [vp]),
             'h264mi_enc_nal_bytes': (i, [vp, vp]),
@@ -56,6 +57,7 @@ def lib():
             'h264mi_enc_frame_bytes': (ctypes.c_size_t, [vp]),
             'h264mi_enc_last_qp': (i, [vp, i]),
             'h264mi_enc_rc_state': (i, [vp, i, vp]),
+            'h264mi_enc_gom_state': (i, [vp, i, vp, i]),
             'h264mi_rc_qstep_to_qp': (i, [i]),
             'h264mi_enc_mbinfo': (i, [vp, i, vp]),
             'h264mi_enc_ref_planes': (i, [vp, i, vp]),
@@ -276,6 +278,20 @@ class BatchEncoder:
         """test hook: stream s's next coded frame fails (0 bytes out, then an IDR)"""
         if self._L.h264mi_enc_inject_error(self._e, s, code) != 0:
             raise RuntimeError('h264mi_enc_inject_error failed')
+
+    def set_gom_exact(self, on):
+        """OpenH264's exact GOM rate control (h264mi_enc_set_gom_exact)"""
+        if self._L.h264mi_enc_set_gom_exact(self._e, 1 if on else 0) != 0:
+            raise RuntimeError('h264mi_enc_set_gom_exact failed')
+
+    def gom_state(self, s=0):
+        """exact GOM mode: the last P frame's per-GOM [QP, slice bits before it, target bits, last coded MB + 1]
+        (h264mi_enc_gom_state)"""
+        G = self._L.h264mi_enc_gom_state(self._e, s, None, 0)
+        out = (ctypes.c_int * (4 * max(G, 1)))()
+        if G < 0 or self._L.h264mi_enc_gom_state(self._e, s, out, 4 * G) != G:
+            raise RuntimeError('h264mi_enc_gom_state failed')
+        return [list(out[4 * g:4 * g + 4]) for g in range(G)]
 
     def frames_skipped(self, s=0):
         return self._L.h264mi_enc_frames_skipped(self._e, s)

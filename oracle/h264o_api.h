@@ -41,6 +41,7 @@ int h264o_table(const char *name, double *out);  /* the oracle's copy of an Open
 /* OpenH264's rate control restated from h264.wasm */
 float h264o_logf(float x);                 /* musl logf (func 483) */
 int h264o_rc_qstep2qp(int32_t qstep);      /* RcConvertQStep2Qp */
+int h264o_enc_gom_state(const H264OEnc *e, int32_t *out, int cap);
 void h264o_enc_set_gom_exact(H264OEnc *e, int enable);  /* MB QPs by OpenH264's GOM rule (funcs 1215 / 1206) */
 void h264o_enc_rc_state(const H264OEnc *e, int32_t out[16]);
 size_t h264o_write_sps(int w, int h, int bitrate, uint8_t *out);

@@ -29,8 +29,8 @@
 #define VGOP_SIZE 8         /* RcInitVGop / RcInitTlWeight: iGopNumberInVGop = 8 >> iDecompositionStages */
 #define WEIGHT_MULTIPLY 2000
 /* Stream syntax OpenH264 writes at the wrapper's parameters, read from the same binary's code
- * (tools/wasm_syntax.py pins each instruction): WelsInitSps (func 280) stores
- * uiLog2MaxFrameNum 15 and uiPocType 2 as one i64 constant (file offset 167929), so the slice header
+ * (tools/wasm_tables.py CODE_CONSTANTS pins each instruction): WelsInitSps (func 280) stores
+ * uiLog2MaxFrameNum 15 and uiPocType 2 as one i64 constant (sps_log2_max_frame_num_and_poc_type, 167923), so the slice header
  * carries a 15-bit frame_num and no POC; the level comes from the level limits at the 60 fps frame
  * rate and the target bitrate (level_idc_for below). */
 #define LOG2_MAX_FRAME_NUM 15
@@ -86,6 +86,8 @@ typedef struct {
     int complexity_index, calc_qp;   /* sl+1348 iComplexityIndexSlice, sl+1352 iCalculatedQpSlice */
     int total_qp, total_mb;          /* sl+1364, sl+1368 */
     uint32_t *gom_sad;      /* rc+132 pCurrentFrameGomSad: the frame's complexity per GOM */
+    int mb_seen, last_coded; /* this frame's MBs counted so far, the last one with bits (-1: none) */
+    int32_t *gom_trace;     /* per GOM of the last P frame {QP, slice bits before it, target bits, last coded MB + 1} */
 } Rc;
 
 struct H264OEnc {
@@ -167,6 +169,7 @@ int h264o_rc_init_qp(int w, int h, int bitrate) {
  * uiLevelIdc unknown, so it becomes level 5.2's MaxBR x 1200. */
 static void rc_init(Rc *rc, int w, int h, int bitrate) {
     uint32_t *g = rc->gom_sad;
+    int32_t *gt = rc->gom_trace;
     memset(rc, 0, sizeof(*rc));
     const int w16 = (w + 15) & ~15, h16 = (h + 15) & ~15;
     rc->mbw = w16 >> 4;
@@ -180,6 +183,7 @@ static void rc_init(Rc *rc, int w, int h, int bitrate) {
     for (int i = 0; i < 17; i++) if (OH_LEVEL_LIMITS[i][0] == 52) rc->max_bitrate = OH_LEVEL_LIMITS[i][4] * 1200;
     rc->skip_en = 1;
     rc->gom_sad = g;
+    rc->gom_trace = gt;
 }
 /* RcUpdateBitrateFps (func 697): float per-frame bits at the 60 fps default, the temporal layer's bit bounds
  * (55 % / 150 % of the GOP's bits at iRcVaryRatio 10, weighted), the skip buffer (50 % of the bitrate) */
@@ -309,6 +313,7 @@ static void rc_picture_init(Rc *rc, int idr, int w, int h) {
     rc->calc_qp = rc->global_qp;
     rc->total_qp = rc->total_mb = 0;
     rc->frame_bits_slice = rc->gom_bits_slice = rc->gom_target_bits = 0;
+    rc->mb_seen = 0; rc->last_coded = -1;
     rc->target_bits_slice = (int)(uint32_t)(uint64_t)(((int64_t)rc->nmb * rc->bits_per_mb + 50) / 100);
 }
 /* WelsRcMbInitGom (func 1215) in exact-GOM mode: at the first MB of every GOM after the first, RcCalculateGomQp
@@ -344,6 +349,8 @@ static int rc_mb_init_gom(Rc *rc, int mb, int idr) {
             else left = (int)(uint32_t)(uint64_t)(((int64_t)(sum / 2) + (int64_t)(int32_t)rc->gom_sad[k + 1] * (int64_t)(uint32_t)left) / sum);
         }
         rc->gom_target_bits = left;
+        int32_t *t = rc->gom_trace + 4 * k;
+        t[0] = rc->calc_qp; t[1] = rc->frame_bits_slice; t[2] = left; t[3] = rc->last_coded + 1;
     }
     return rc->calc_qp;
 }
@@ -351,7 +358,8 @@ static int rc_mb_init_gom(Rc *rc, int mb, int idr) {
 static void rc_mb_update(Rc *rc, int bits, int qp) {
     rc->frame_bits_slice += bits;
     rc->gom_bits_slice += bits;
-    if (bits > 0) { rc->total_qp += qp; rc->total_mb++; }
+    if (bits > 0) { rc->total_qp += qp; rc->total_mb++; rc->last_coded = rc->mb_seen; }
+    rc->mb_seen++;
 }
 /* WelsRcPictureInfoUpdateGom (func 1218) after a coded frame: slice_bytes = the slice NAL (start code and
  * emulation prevention included; the parameter sets are another layer). RcUpdatePictureQpBits, the R-Q model
@@ -1003,6 +1011,7 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
     e->rowbits = (int64_t *)calloc((size_t)e->mbh, sizeof(int64_t));
     e->prev_src = (uint8_t *)calloc((size_t)e->cw * e->ch, 1);
     e->rc.gom_sad = (uint32_t *)calloc((size_t)e->mbw * e->mbh, sizeof(uint32_t));
+    e->rc.gom_trace = (int32_t *)calloc(4 * (size_t)e->mbw * e->mbh, sizeof(int32_t));
     rc_init(&e->rc, w, h, bitrate);  /* frame skipping on: the wrapper leaves bEnableFrameSkip at its default */
     e->first = 1;
     e->idr_pic_id = 0;
@@ -1011,7 +1020,7 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
 void h264o_enc_destroy(H264OEnc *e) {
     if (!e) return;
     for (int p = 0; p < 3; p++) { free(e->src[p]); free(e->rec[p]); free(e->ref[p]); }
-    free(e->prev_src); free(e->rc.gom_sad);
+    free(e->prev_src); free(e->rc.gom_sad); free(e->rc.gom_trace);
     free(e->mbs); free(e->rowqp); free(e->rowbits); free(e);
 }
 /* bEnableFrameSkip (on by default, as the wrapper leaves it): off, no frame is skipped, the VBV check is not
@@ -1028,6 +1037,13 @@ void h264o_enc_rc_state(const H264OEnc *e, int32_t out[16]) {
     out[5] = (int32_t)r->fullness; out[6] = r->continual_skip; out[7] = (int32_t)r->frame_cmplx; out[8] = r->min_frame_qp;
     out[9] = r->max_frame_qp; out[10] = r->bpf; out[11] = r->pframe_num; out[12] = r->idr_num; out[13] = r->skip_flag;
     out[14] = r->remaining_weights; out[15] = r->frame_coded_in_vgop;
+}
+/* exact GOM mode: the last P frame's per-GOM {QP, slice bits before it, target bits, last coded MB + 1} (4 int32
+ * per GOM, at most cap values); returns the GOM count */
+int h264o_enc_gom_state(const H264OEnc *e, int32_t *out, int cap) {
+    const int G = e->rc.gom_count;
+    for (int i = 0; i < 4 * G && i < cap; i++) out[i] = e->rc.gom_trace[i];
+    return G;
 }
 int h264o_enc_frames_skipped(const H264OEnc *e) { return e ? e->skipped : 0; }
 void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]) {

@@ -25,6 +25,7 @@ class Oracle:
         L.h264o_logf.restype = ctypes.c_float
         L.h264o_enc_set_gom_exact.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.h264o_enc_rc_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.h264o_enc_gom_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.h264o_write_sps.restype = ctypes.c_size_t
         L.h264o_write_sps.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
         L.h264o_write_pps.restype = ctypes.c_size_t
@@ -86,6 +87,13 @@ class OEnc:
         out = (ctypes.c_int32 * 16)()
         self.L.h264o_enc_rc_state(self.e, out)
         return dict(zip(self.RC_FIELDS, list(out)))
+
+    def gom_state(self):
+        """exact GOM mode: the last P frame's per-GOM [QP, slice bits before it, target bits, last coded MB + 1]"""
+        G = self.L.h264o_enc_gom_state(self.e, None, 0)
+        out = (ctypes.c_int32 * (4 * max(G, 1)))()
+        self.L.h264o_enc_gom_state(self.e, out, 4 * G)
+        return [list(out[4 * g:4 * g + 4]) for g in range(G)]
 
     def recon(self):
         out = np.zeros(self.w * self.h * 3 // 2, np.uint8)

@@ -207,3 +207,45 @@ def test_capi_decoder_memory_1080p(gpu_lib, oracle):
     dec.close()
     assert 0 < capi < 64 << 20, capi
     assert batch > capi, (batch, capi)
+
+
+@pytest.mark.parametrize('w,h,br,skip,S,nf', [(1920, 1080, 8000000, False, 2, 6), (1920, 1080, 20000000, True, 2, 5),
+                                              (1280, 720, 2000000, False, 2, 5), (352, 288, 500000, False, 4, 6)],
+                         ids=['1080p_8m', '1080p_20m_skip', '720p_odd_gom', 'cif_narrow'])
+def test_exact_gom_rc_vs_oracle(gpu_lib, oracle, w, h, br, skip, S, nf):
+    """OpenH264's GOM rate control exactly (h264mi_enc_set_gom_exact; oracle h264o_enc_set_gom_exact): every P
+    frame's GOM takes its QP from the bits of every MB coded before it (WelsRcMbInitGom, h264.wasm func 1215).
+    GPU bytes, RC state and every GOM's {QP, slice bits before it, target bits} == oracle, GOMs of 2 MB rows (1080p, 720p whose last GOM has one row) and of 1 row
+    (352x288: fewer than 31 MBs wide); the MB QPs really vary inside pictures"""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    gs = [SyntheticStream(5 + s, w, h) for s in range(S)]
+    enc = h264mi.BatchEncoder(w, h, br, S)
+    enc.set_gom_exact(True)
+    enc.set_frame_skip(skip)
+    oes = [oracle.encoder(w, h, br) for _ in range(S)]
+    od = oracle.decoder()
+    qps = set()
+    for oe in oes:
+        oe.set_gom_exact(True)
+        oe.set_frame_skip(skip)
+    for t in range(nf):
+        fr = [np.ascontiguousarray(g.frame(t)) for g in gs]
+        enc.encode(torch.from_numpy(np.stack(fr)).cuda())
+        n = enc.nal_sizes()
+        for s in range(S):
+            ref = oes[s].encode(fr[s])
+            assert n[s] == len(ref) and (n[s] == 0 or enc.nal_bytes(s, n[s]) == ref), f'frame {t} stream {s}'
+            assert enc.rc_state(s) == oes[s].rc_state(), f'frame {t} stream {s}'
+            if t > 0 and ref and not enc.rc_state(s)['skipped']:  # per GOM: QP, bits before it, target, last MB
+                assert enc.gom_state(s) == oes[s].gom_state(), f'frame {t} stream {s}'
+            if s == 0 and ref:
+                rc, _, _, _ = od.decode(ref)
+                assert rc == 1
+                mi = np.zeros(((w + 15) // 16) * ((h + 15) // 16) * 8, np.int32)
+                oracle.L.h264o_dec_mbinfo(od.d, mi.ctypes.data)
+                if t > 0:
+                    qps.add(len(set(mi.reshape(-1, 8)[:, 1].tolist())))
+    assert max(qps) > 1, qps
+    enc.close()

@@ -91,7 +91,7 @@ def worker_window(args):
     enc_i mode), every frame encoded and -- except in enc_i mode -- decoded by the oracle. Returns the time of
     the encode and decode calls of frames first..T (the GPU's timed window: like-for-like content) and the
     sha256 of frame T's NAL bytes and decoded picture (the timed pipeline's last frame, checked after the
-    timed region)."""
+    timed region), and the pid of the process that ran it (window() adds busy time per real process)."""
     stream, w, h, bitrate, T, clip, mode, first = args
     sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
     import numpy as np
@@ -127,20 +127,21 @@ def worker_window(args):
             'pic': hashlib.sha256(pic.tobytes()).hexdigest() if mode != 'enc_i' else None}
     O.h264o_enc_destroy(e)
     O.h264o_dec_destroy(d)
-    return stream, t_enc, t_dec, T + 1 - first, last
+    return stream, t_enc, t_dec, T + 1 - first, last, os.getpid()
 
 
 def window(streams, w, h, bitrate, T, clip, mode, first, procs):
     """worker_window over the given streams on `procs` processes; each process's busy time is the sum over
-    its streams, the rate is all timed frames / the busiest process (as run())"""
+    the streams it really ran (the pool hands jobs out dynamically: accounted by the worker's pid), the rate is
+    all timed frames / the busiest process (as run())"""
     jobs = [(sid, w, h, bitrate, T, clip, mode, first) for sid in streams]
     with mp.get_context('spawn').Pool(max(1, min(procs, len(jobs)))) as pool:
         res = pool.map(worker_window, jobs, chunksize=1)
-    per = [0.0] * max(1, min(procs, len(jobs)))
-    per_e = list(per)
-    for k, r in enumerate(res):  # the pool's order is not the assignment; this spreads streams evenly
-        per[k % len(per)] += r[1] + r[2]
-        per_e[k % len(per_e)] += r[1]
+    busy, busy_e = {}, {}
+    for r in res:
+        busy[r[5]] = busy.get(r[5], 0.0) + r[1] + r[2]
+        busy_e[r[5]] = busy_e.get(r[5], 0.0) + r[1]
+    per, per_e = list(busy.values()), list(busy_e.values())
     counted = sum(r[3] for r in res)
     return {'value': counted / max(per) if max(per) > 0 else None, 'encode_only': counted / max(per_e) if max(per_e) > 0 else None,
             'unit': 'frames/s', 'cores': len(per), 'frames': f'{first}..{T}', 'streams': len(jobs), 'timed_frames': counted,
