@@ -7,9 +7,9 @@ stream (captured in the warmup) and the last timed frame of every stream (captur
 region); parity with OpenH264 itself is partial. A failed check prints value null and exits 1.
 
 Default workload (the metric; at N > 1 also BASELINE.json configs[4]'s NAL gather): every rank owns
-S streams (default 32: the GPU's 1080p30 throughput comes from concurrent independent streams, SURVEY.md
-§7; at 32 streams a frame step of all of them takes ~7.7 ms, inside the 33 ms of a 30 fps frame
-interval, so every stream runs in real time; 64-128 streams add 10-20 %, DESIGN.md §5 Capacity). One
+S streams (default 128: the GPU's 1080p30 throughput comes from concurrent independent streams, SURVEY.md
+§7; at 128 streams a frame step of all of them takes ~24 ms, inside the 33 ms of a 30 fps frame
+interval, so every stream runs in real time; 32 streams give ~20 % less, DESIGN.md §5 Capacity). One
 step = one frame of each of them: GPU encode (libh264mi batch encoder,
 IPPP, intra period 0, the wrapper's parameters, 1 Mbps) and GPU decode of exactly the NAL units
 produced, plus (N > 1) the gather of those NAL units to rank 0 over RCCL. Frames are encoded on one
@@ -93,16 +93,23 @@ def parse():
                     help='streamed reconstruction (h264mi_dec_set_streamed; -1: the library\'s automatic choice, which '
                          'leaves a 32-stream decoder unstreamed: its 4352 waiting reconstruction waves would hold the CUs '
                          'the encoder needs while a long slice parses -- profiles/round4/timeline_streamed_tail.txt)')
+    ap.add_argument('--gom-exact', action='store_true',
+                    help='P-frame QPs by OpenH264\'s exact GOM rate control (H264MI_GOM_EXACT=1 for the encoders and the '
+                         'oracle); default: this project\'s MB-row plan (DESIGN.md §3.6)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=7)
     ap.add_argument('--parity-frames', type=int, default=4, help='frames of stream 0 checked against the oracle before timing')
     ap.add_argument('--no-traffic', action='store_true', help='skip the rocprofv3 --pmc passes that measure roofline.traffic')
     ap.add_argument('--traffic-probe', action='store_true', help=argparse.SUPPRESS)  # child of measure_traffic()
     a = ap.parse_args()
+    if a.gom_exact:  # before any child process starts and before the library is loaded
+        os.environ['H264MI_GOM_EXACT'] = '1'
     if a.config == 2:
         a.width, a.height = a.width or 1280, a.height or 720
     a.width, a.height = a.width or 1920, a.height or 1080
-    a.streams = a.streams or {2: 8, 3: 1, 4: 8, 5: 4}.get(a.config, 32)
+    # the metric workload: 128 streams per GPU (round 6, profiles/round6/sweep_streams.txt: 32 streams 4296-4320
+    # frames/s, 64 4820, 96 5079, 128 5108-5323, 192 5275, 256 5181-5362 -- the pipeline fills the chip from ~128)
+    a.streams = a.streams or {2: 8, 3: 1, 4: 8, 5: 4}.get(a.config, 128)
     a.group = a.group or (16 if a.config == 4 else 4)
     # one encoder: two of 16 streams each on their own HIP streams measured within noise of it (3826-3922 vs
     # 3738-3902 frames/s over 8 runs, profiles/round4/ab_enc_groups*.txt) and halve the per-launch roofline
@@ -113,8 +120,10 @@ def parse():
         # run best on the fewest CUs that take them in two rounds -- 16 CUs 4517-4546 frames/s, 20 4512-4521,
         # 24 4501, 32 4485-4492, 40 4211-4230; 12 and 8 (three and four rounds) drop to 3655. 20 keeps a round's
         # margin: 20 CUs per 128 slices, in steps of 4 (smaller calls keep the earlier 24)
+        # Round 6 at 512 and 1024 slices (128 / 256 streams): 32 CUs (four slice waves each: 4 and 8 full rounds)
+        # beat 24 (5108 / 5181), 28 (5091), 36 (4904), 40 (4969 / 5107), 48 (4984) and 80 (4309 / 4336)
         sl = a.streams * a.group
-        a.parse_cus = (-(-sl * 20 // (128 * 4)) * 4 if sl >= 128 else 24) if a.config in (0, 3, 5) else 0
+        a.parse_cus = ((20 if sl <= 128 else 24 if sl < 512 else 32) if sl >= 128 else 24) if a.config in (0, 3, 5) else 0
     # Hardware queues per process: the pipeline drives the encoder stream, the reconstruction stream and
     # the decoder's entropy-decoding streams (runtime_dec.inc); with HIP's default of 4 queues parse
     # streams share queues and their kernels serialise. Set before the HIP runtime initialises.
@@ -266,6 +275,56 @@ def measure_traffic(a):
                  f'loads, so 2 x FETCH_SIZE is an upper bound on its reads and the raw counters ({raw / 1e6:.1f} MB) a lower bound')
 
 
+PARSE_SQ = ('SQ_WAVE_CYCLES', 'SQ_INSTS_SALU', 'SQ_INSTS_VALU', 'SQ_INSTS_BRANCH', 'SQ_INSTS_SMEM', 'SQ_INSTS_LDS',
+            'SQ_WAIT_ANY', 'SQ_ACTIVE_INST_ANY')  # one pass: 8 SQ counters (the block's limit)
+
+
+def measure_parse_mix(a):
+    """dec_parse_kernel's instruction mix and issue rate, measured in this run: one rocprofv3
+    --pmc pass over a short child bench of the same workload (--steps 4 --warmup 4, no CPU leg, no PMC of its
+    own; the first dispatch, the IDR's I slices, is left out). A slice is one wave whose CAVLC chain issues at
+    most one instruction per quad-cycle (~4.3 cycles per independent SALU op on gfx950), so
+    issue_frac = instructions / SQ_WAVE_CYCLES (quad-cycles) is the fraction of that per-wave issue bound the
+    slices reach; the rest is dependency latency (taken branches, readlane -> SALU, LDS) and waits."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    if not shutil.which('rocprofv3'):
+        return {'note': 'rocprofv3 not found'}
+    work = tempfile.mkdtemp(prefix='h264mi_pmc_parse_', dir='/tmp')
+    cmd = ['rocprofv3', '--pmc', *PARSE_SQ, '-d', work, '-o', 'run', '--output-format', 'csv', '--', sys.executable,
+           os.path.abspath(__file__), '--no-cpu-baseline', '--no-traffic', '--steps', '4', '--warmup', '4', '--clip', '8',
+           '--config', str(a.config), '--streams', str(a.streams), '--width', str(a.width), '--height', str(a.height),
+           '--bitrate', str(a.bitrate), '--group', str(a.group), '--parse-cus', str(a.parse_cus),
+           '--parse-streams', str(a.parse_streams), '--enc-groups', str(a.enc_groups), '--dec-groups', str(a.dec_groups)]
+    try:
+        subprocess.run(cmd, cwd='/tmp', env=dict(os.environ, TMPDIR='/tmp'), capture_output=True, text=True, timeout=240)
+    except Exception as e:  # reported, never replaced by a stored figure
+        shutil.rmtree(work, ignore_errors=True)
+        return {'note': f'PMC pass failed: {e!r}'}
+    per = {}
+    for f in glob.glob(os.path.join(work, '**', '*counter_collection.csv'), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if 'dec_parse_kernel' in r['Kernel_Name']:
+                d = per.setdefault(int(r['Dispatch_Id']), {})
+                d[r['Counter_Name']] = d.get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
+    shutil.rmtree(work, ignore_errors=True)
+    ks = sorted(per)[1:]
+    if not ks:
+        return {'note': 'no dec_parse_kernel dispatches recorded'}
+    t = {c: sum(per[k].get(c, 0.0) for k in ks) for c in PARSE_SQ}
+    insts = sum(t[c] for c in PARSE_SQ[1:6])
+    wc = t['SQ_WAVE_CYCLES'] or 1.0
+    return {'dispatches': len(ks), 'instructions': insts, 'wave_quad_cycles': t['SQ_WAVE_CYCLES'],
+            'issue_frac': insts / wc, 'salu_share': t['SQ_INSTS_SALU'] / max(insts, 1.0),
+            'branch_share': t['SQ_INSTS_BRANCH'] / max(insts, 1.0), 'active_frac': t['SQ_ACTIVE_INST_ANY'] / wc,
+            'wait_frac': t['SQ_WAIT_ANY'] / wc,
+            'note': 'rocprofv3 --pmc ' + ' '.join(PARSE_SQ) + ' over dec_parse_kernel dispatches 2.. of a 4 + 4-step child '
+                    'bench of this workload; instructions = SALU + VALU + BRANCH + SMEM + LDS; issue_frac = instructions '
+                    '/ SQ_WAVE_CYCLES (quad-cycles: 1.0 = one instruction per 4 cycles per wave, the per-wave issue bound)'}
+
+
 def oracle_hashes(a, mode, first):
     """the oracle's sha256 of the first frames of this rank's streams first..first+S-1 (N > 1 ranks;
     child process, no GPU): {str(stream id): [{'nal', 'pic'}, ...]}"""
@@ -390,8 +449,11 @@ def main():
         shashes, last = oracle_hashes(a, mode, rank * a.streams)
     a.traffic_kernel = 'dec_recon_kernel' if a.config == 4 else 'enc_mb_kernel'
     a.traffic_measured = (None, 'not measured (--no-traffic or N > 1)')
+    a.parse_mix = None
     if rank == 0 and world == 1 and not a.no_traffic:
         a.traffic_measured = measure_traffic(a)
+        if a.config in (0, 3, 5) and not a.no_decode:
+            a.parse_mix = measure_parse_mix(a)
     import numpy as np
     import torch
     import h264mi
@@ -705,7 +767,11 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
         rms, rn = [sum(x) for x in zip(*[dec.kernel_time(0) for dec in decs])]
         pms, pn = [sum(x) for x in zip(*[dec.kernel_time(1) for dec in decs])]
         kern['dec_recon_kernel'] = {'avg_ms': rms / max(rn, 1), 'launches': rn}
-        kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': Sd * G}
+        kern['dec_parse_kernel'] = {'avg_ms': pms / max(pn, 1), 'launches': pn, 'slices_per_launch': Sd * G,
+                                    # the parse launches' summed duration over the timed region's wall time (they run
+                                    # beside the encoder and the reconstruction on reserved CUs, so this is not additive)
+                                    'busy_share_of_timed_wall': pms / (elapsed * 1e3) if elapsed > 0 else None,
+                                    'sq': a.parse_mix}
         if os.environ.get('H264MI_PARSE_PROF'):  # diagnostic: the slices' own duration (wave start to end)
             dec = decs[0]
             nsl = Sd * G * dec.ring_groups()
@@ -731,6 +797,7 @@ def bench_encode(a, torch, np, h264mi, SyntheticStream, NalGather, stream_ids, d
                        + (f', decode batches of {G} frames' if decode else '') + ('; NAL gather to rank 0 at N>1' if a.config in (0, 5) else ''),
            'baseline_config': {0: f'metric (configs[2] x {S} streams)', 2: 'configs[1]', 3: 'configs[2]', 5: 'configs[4]'}[a.config],
            'width': W, 'height': H, 'streams_per_gpu': S, 'bitrate': a.bitrate, 'group': G, 'frame_skip': False,
+           'p_frame_qp': 'OpenH264 exact GOM' if a.gom_exact else 'MB-row plan (DESIGN.md §3.6)',
            'parse_cus': a.parse_cus, 'recon_cus': a.recon_cus, 'parse_streams': a.parse_streams,
            'streamed_recon': streamed_mode, 'tail_streamed': tail_streamed, 'recon_gate': bool(a.recon_gate), 'enc_groups': EG, 'dec_groups': DG,
            'parallelism': f'streams x{world} (weak)'}

@@ -22,6 +22,13 @@ import multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def gom_exact():
+    """the P-frame QP rule of the GPU encoders this baseline is compared with: OpenH264's exact GOM rate control
+    when H264MI_GOM_EXACT=1 (bench.py --gom-exact; the library reads the same variable), else the MB-row plan"""
+    v = os.environ.get('H264MI_GOM_EXACT', '0').strip()
+    return 1 if v.isdigit() and int(v) != 0 else 0  # as the library's atoi(...) != 0 for plain digits
+
+
 def worker(args):
     stream, w, h, bitrate, nframes, mode, nhash = args
     sys.path.insert(0, os.path.join(ROOT, 'openh264-wasm_amd'))
@@ -35,6 +42,7 @@ def worker(args):
     frames = [np.ascontiguousarray(S.frame(t)) for t in range(nframes)]
     e = vp(O.h264o_enc_create(w, h, bitrate))
     O.h264o_enc_set_frame_skip(e, 0)  # as bench.py's GPU encoder: every frame coded
+    O.h264o_enc_set_gom_exact(e, gom_exact())
     d = vp(O.h264o_dec_create())
     out = np.zeros(w * h * 4, np.uint8)
     pic = np.zeros(w * h * 3 // 2, np.uint8)
@@ -104,6 +112,7 @@ def worker_window(args):
     frames = [np.ascontiguousarray(S.frame(t)) for t in range(min(clip, T + 1))]
     e = vp(O.h264o_enc_create(w, h, bitrate))
     O.h264o_enc_set_frame_skip(e, 0)
+    O.h264o_enc_set_gom_exact(e, gom_exact())
     d = vp(O.h264o_dec_create())
     out = np.zeros(w * h * 4, np.uint8)
     pic = np.zeros(w * h * 3 // 2, np.uint8)
