@@ -42,6 +42,11 @@ int h264o_table(const char *name, double *out);  /* the oracle's copy of an Open
 float h264o_logf(float x);                 /* musl logf (func 483) */
 int h264o_rc_qstep2qp(int32_t qstep);      /* RcConvertQStep2Qp */
 int h264o_enc_gom_state(const H264OEnc *e, int32_t *out, int cap);
+/* intra mode decision pieces, for tests: AnalysisVaaInfoIntra of a 16x16 source block, the
+ * Intra4x4 choice of one block from its nine mode costs and availability index, the pinned constants */
+int h264o_vaa_intra_var(const uint8_t *src, int stride);
+int h264o_i4_choose(const int32_t c[9], int avail_index, int32_t *cost);
+void h264o_md_constants(int32_t out[3]);
 void h264o_enc_set_gom_exact(H264OEnc *e, int enable);  /* MB QPs by OpenH264's GOM rule (funcs 1215 / 1206) */
 void h264o_enc_rc_state(const H264OEnc *e, int32_t out[16]);
 size_t h264o_write_sps(int w, int h, int bitrate, uint8_t *out);

@@ -28,6 +28,10 @@
 #define IDR_QP_WINDOW 3     /* RcCalculateIdrQp: the IDR's frame QP window (func 1226) */
 #define VGOP_SIZE 8         /* RcInitVGop / RcInitTlWeight: iGopNumberInVGop = 8 >> iDecompositionStages */
 #define WEIGHT_MULTIPLY 2000
+/* intra mode decision (tools/wasm_tables.py CODE_CONSTANTS md_*) */
+#define OH_VAA_I4_THRESHOLD 149  /* WelsMdIntraFinePartitionVaa: I4x4 tried when the VAA variance is above this */
+#define OH_I4_MODE_BITS_SHIFT 2  /* a mode other than the predicted one costs lambda << 2 */
+#define OH_I4_MB_OVERHEAD 24     /* the I4x4 MB costs its blocks + 24 lambda */
 /* Stream syntax OpenH264 writes at the wrapper's parameters, read from the same binary's code
  * (tools/wasm_tables.py CODE_CONSTANTS pins each instruction): WelsInitSps (func 280) stores
  * uiLog2MaxFrameNum 15 and uiPocType 2 as one i64 constant (sps_log2_max_frame_num_and_poc_type, 167923), so the slice header
@@ -445,6 +449,11 @@ static void rc_plan_rows(H264OEnc *e) {
     int64_t mean = sum / e->mbh;
     for (int r = 0; r < e->mbh; r++) e->rowqp[r] = h264o_rc_row_delta(e->rowbits[r], mean);
 }
+/* the intra mode decision's constants for tests/test_oracle_golden.py: {VAA threshold, mode bits shift, I4x4 MB
+ * overhead} (pinned against the h264.wasm fixture, tools/wasm_tables.py md_*) */
+void h264o_md_constants(int32_t out[3]) {
+    out[0] = OH_VAA_I4_THRESHOLD; out[1] = OH_I4_MODE_BITS_SHIFT; out[2] = OH_I4_MB_OVERHEAD;
+}
 /* oracle RC constants for tests/test_oracle_golden.py (pinned against the h264.wasm fixture) */
 void h264o_rc_constants(int32_t out[8]) {
     out[0] = RC_FPS; out[1] = QP_MIN; out[2] = QP_MAX; out[3] = FRAME_DQP_LOWER; out[4] = FRAME_DQP_UPPER;
@@ -463,6 +472,14 @@ int h264o_table(const char *name, double *out) {
     else if (!strcmp(name, "logf_table")) { for (int i = 0; i < 32; i++) out[n++] = OH_LOGF_T[i / 2][i % 2]; }
     else if (!strcmp(name, "logf_poly")) { for (int i = 0; i < 4; i++) out[n++] = OH_LOGF_P[i]; }
     else if (!strcmp(name, "rc_tl_weight")) { for (int i = 0; i < 16; i++) out[n++] = OH_RC_TL_WEIGHT[i / 4][i % 4]; }
+    else if (!strcmp(name, "i16_avail_modes")) { for (int i = 0; i < 40; i++) out[n++] = OH_I16_AVAIL[i / 5][i % 5]; }
+    else if (!strcmp(name, "i16_mode_map")) { for (int i = 0; i < 7; i++) out[n++] = OH_I16_MAP[i]; }
+    else if (!strcmp(name, "chroma_avail_modes")) { for (int i = 0; i < 40; i++) out[n++] = OH_CHROMA_AVAIL[i / 5][i % 5]; }
+    else if (!strcmp(name, "chroma_mode_map")) { for (int i = 0; i < 7; i++) out[n++] = OH_CHROMA_MAP[i]; }
+    else if (!strcmp(name, "i4_avail_index")) { for (int i = 0; i < 256; i++) out[n++] = OH_I4_AVAIL_IDX[i / 16][i % 16]; }
+    else if (!strcmp(name, "i4_avail_count")) { for (int i = 0; i < 16; i++) out[n++] = OH_I4_COUNT[i]; }
+    else if (!strcmp(name, "i4_avail_modes")) { for (int i = 0; i < 256; i++) out[n++] = OH_I4_MODES[i / 16][i % 16]; }
+    else if (!strcmp(name, "i4_mode_map")) { for (int i = 0; i < 16; i++) out[n++] = OH_I4_MAP[i]; }
     else if (!strcmp(name, "level_limits")) { for (int i = 0; i < 17 * 6; i++) out[n++] = OH_LEVEL_LIMITS[i / 6][i % 6]; }
     else return -1;
     return n;
@@ -607,17 +624,6 @@ static int satd16x16(const uint8_t *src, int ss, const uint8_t *pred, int ps) {
         }
     return s;
 }
-static int satd8x8(const uint8_t *src, int ss, const uint8_t *pred, int ps) {
-    int s = 0, d[16];
-    for (int by = 0; by < 2; by++)
-        for (int bx = 0; bx < 2; bx++) {
-            for (int y = 0; y < 4; y++)
-                for (int x = 0; x < 4; x++)
-                    d[4 * y + x] = src[(4 * by + y) * ss + 4 * bx + x] - pred[(4 * by + y) * ps + 4 * bx + x];
-            s += satd4(d);
-        }
-    return s;
-}
 static int count_nz(const int16_t *c, int n) { int k = 0; for (int i = 0; i < n; i++) k += c[i] != 0; return k; }
 
 /* Luma 4x4 residual: forward transform + quantisation into scan-ordered levels; returns the
@@ -664,26 +670,45 @@ static void encode_chroma(H264OEnc *e, MBInfo *mb, int mbx, int mby, uint8_t pre
         }
     }
 }
-static int best_chroma_mode(H264OEnc *e, int mbx, int mby, IntraNb nb[2], uint8_t pred[2][64]) {
-    int cs = e->cw / 2, best = -1, bc = 0;
+/* sum of absolute differences of a w x h block (pfSampleSad: the mode decision's cost at the wrapper's settings) */
+static int sad_blk(const uint8_t *src, int ss, const uint8_t *pred, int ps, int w, int h) {
+    int s = 0;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) s += iabs(src[y * ss + x] - pred[y * ps + x]);
+    return s;
+}
+/* bits of ue(v) (BsSizeUE) */
+static int ue_bits(int v) { int n = 0; while (((unsigned)v + 1) >> (n + 1)) n++; return 2 * n + 1; }
+/* the MB's neighbour flags as OpenH264's MB cache holds them (one slice per picture): 1 left, 2 top, 4 top-left,
+ * 8 top-right (uiNeighborAvail, func 246 125527) */
+static int mb_nb_flags(int mbx, int mby, int mbw) {
+    return (mbx > 0) | ((mby > 0) << 1) | ((mbx > 0 && mby > 0) << 2) | ((mby > 0 && mbx + 1 < mbw) << 3);
+}
+/* WelsMdIntraChroma (h264.wasm func 312) with pfMdCost = SAD: the modes of OH_CHROMA_AVAIL[flags & 7]
+ * in that order, cost = SAD(Cb) + SAD(Cr) + lambda * ue bits of the syntax mode, the first minimum wins (strict <).
+ * The internal DC_L / DC_T / DC_128 modes are the standard's DC for those neighbours. */
+static int best_chroma_mode(H264OEnc *e, int mbx, int mby, IntraNb nb[2], uint8_t pred[2][64], int lam) {
+    const int cs = e->cw / 2;
+    const int8_t *row = OH_CHROMA_AVAIL[mb_nb_flags(mbx, mby, e->mbw) & 7];
+    int best = 0x7fffffff, bm = OH_CHROMA_MAP[row[0]];
     uint8_t p[2][64];
-    for (int m = 0; m < 4; m++) {
-        if (!pred_chroma_avail(&nb[0], m)) continue;
-        int c = 0;
+    for (int i = 0; i < row[4]; i++) {
+        const int m = OH_CHROMA_MAP[row[i]];
+        int c = lam * ue_bits(m);
         for (int pl = 0; pl < 2; pl++) {
             pred_chroma(&nb[pl], m, p[pl]);
-            c += satd8x8(e->src[1 + pl] + mby * 8 * cs + mbx * 8, cs, p[pl], 8);
+            c += sad_blk(e->src[1 + pl] + mby * 8 * cs + mbx * 8, cs, p[pl], 8, 8, 8);
         }
-        if (best < 0 || c < bc) { best = m; bc = c; memcpy(pred, p, sizeof(p)); }
+        if (c < best) { best = c; bm = m; memcpy(pred, p, sizeof(p)); }
     }
-    return best;
+    return bm;
 }
 static void chroma_intra(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
     IntraNb nb[2];
     int cs = e->cw / 2;
     for (int pl = 0; pl < 2; pl++) get_nb16(e->rec[1 + pl], cs, mbx * 8, mby * 8, 8, mby > 0, mbx > 0, &nb[pl]);
     uint8_t pred[2][64];
-    mb->cmode = best_chroma_mode(e, mbx, mby, nb, pred);
+    mb->cmode = best_chroma_mode(e, mbx, mby, nb, pred, LAMBDA[mb->qp]);
     encode_chroma(e, mb, mbx, mby, pred, 1);
 }
 
@@ -737,42 +762,123 @@ static void encode_i16(H264OEnc *e, MBInfo *mb, int mbx, int mby, int mode, cons
     }
 }
 
-/* Intra MB decision for I slices: I16x16 vs I4x4. */
+/* WelsMdI16x16 (h264.wasm func 313) with pfMdCost = SAD: the modes of OH_I16_AVAIL[flags & 7] in that order, cost
+ * = SAD + lambda * ue bits of the syntax mode, the first minimum wins. Returns the syntax mode. */
+static int i16_best_oh(H264OEnc *e, int mbx, int mby, const IntraNb *nb, int lam, int *cost, uint8_t pred[256]) {
+    const uint8_t *src = e->src[0] + mby * 16 * e->cw + mbx * 16;
+    const int8_t *row = OH_I16_AVAIL[mb_nb_flags(mbx, mby, e->mbw) & 7];
+    int best = 0x7fffffff, bm = OH_I16_MAP[row[0]];
+    uint8_t p[256];
+    for (int i = 0; i < row[4]; i++) {
+        const int m = OH_I16_MAP[row[i]];
+        pred16x16(nb, m, p);
+        const int c = sad_blk(src, e->cw, p, 16, 16, 16) + lam * ue_bits(m);
+        if (c < best) { best = c; bm = m; memcpy(pred, p, 256); }
+    }
+    *cost = best;
+    return bm;
+}
+/* AnalysisVaaInfoIntra (func 854): the variance of the source MB's sixteen 4x4 means (sum >> 4),
+ * sum of squares - (sum^2 >> 4) */
+int h264o_vaa_intra_var(const uint8_t *src, int ss) {
+    uint32_t sum = 0, sq = 0;
+    for (int by = 0; by < 4; by++)
+        for (int bx = 0; bx < 4; bx++) {
+            uint32_t t = 0;
+            for (int y = 0; y < 4; y++) for (int x = 0; x < 4; x++) t += src[(4 * by + y) * ss + 4 * bx + x];
+            t = (t & 0xfff0u) >> 4;
+            sum += t; sq += t * t;
+        }
+    return (int)(sq - ((sum * sum) >> 4));
+}
+/* WelsMdI4x4Fast's choice for one block (inlined in func 774, 475164-476768): c[m] = SAD + (m == predicted mode ?
+ * lambda : 4 lambda) for syntax mode m. Blocks whose availability gives 7 or 9 modes take the fast search -- DC, H
+ * and V first, then the directional modes beside the better of V / H -- the others try their modes in the table's
+ * order; the first minimum wins everywhere (strict <). Returns the mode, *cost its cost. */
+int h264o_i4_choose(const int c[9], int avail_index, int *cost) {
+    const int cnt = OH_I4_COUNT[avail_index];
+    int best, m;
+    if (cnt == 7 || cnt == 9) {
+        const int hb = c[1] < c[2];
+        best = hb ? c[1] : c[2]; m = hb ? 1 : 2;
+        if (c[0] < best) { best = c[0]; m = 0; }
+        if (c[0] < c[1]) {
+            if (cnt == 9) {
+                if (c[5] < best) { best = c[5]; m = 5; }
+                if (best > c[7]) { best = c[7]; m = 7; }
+                if (!(c[0] <= c[7] && c[0] <= c[5])) {
+                    if (c[5] < c[7]) { if (c[4] < best) { best = c[4]; m = 4; } }
+                    else if (c[3] < best) { best = c[3]; m = 3; }
+                }
+            } else {
+                if (c[4] < best) { best = c[4]; m = 4; }
+                if (c[5] < best) { best = c[5]; m = 5; }
+            }
+        } else {
+            if (c[6] < best) { best = c[6]; m = 6; }
+            if (best > c[8]) { best = c[8]; m = 8; }
+            if (!(c[6] >= c[1] && c[8] >= c[1])) {
+                if (c[8] > c[6]) { if (c[4] < best) { best = c[4]; m = 4; } }
+                else if (cnt == 9 && c[3] < best) { best = c[3]; m = 3; }
+            }
+        }
+    } else {
+        best = 0x7fffffff; m = 2;
+        for (int i = 0; i < cnt; i++) {
+            const int mm = OH_I4_MAP[OH_I4_MODES[avail_index][i]];
+            if (c[mm] < best) { best = c[mm]; m = mm; }
+        }
+    }
+    *cost = best;
+    return m;
+}
+/* WelsMdIntraMb (func 439) for I slices: I16x16 (func 313), then -- WelsMdIntraFinePartitionVaa, func 774 -- the
+ * Intra4x4 search only when the source MB's VAA variance is above 149: blocks in decoding order, each coded and
+ * reconstructed as chosen (the next block predicts from it), the search stops as soon as the blocks' cost reaches
+ * the I16x16 cost, and I4x4 wins when its blocks + 24 lambda cost less. */
 static void encode_intra_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
     int lam = LAMBDA[mb->qp];
     IntraNb nb;
     get_nb16(e->rec[0], e->cw, mbx * 16, mby * 16, 16, mby > 0, mbx > 0, &nb);
     uint8_t p16[256];
     int c16;
-    int m16 = i16_best(e, mbx, mby, &nb, &c16, p16);
-    /* I4x4 trial with progressive reconstruction and exact early termination */
+    int m16 = i16_best_oh(e, mbx, mby, &nb, lam, &c16, p16);
     MBInfo t = *mb;
     t.type = MBT_I4;
-    int cost4 = 24 * lam, won = 1;
     const uint8_t *src = e->src[0] + mby * 16 * e->cw + mbx * 16;
     uint8_t *dst = e->rec[0] + mby * 16 * e->cw + mbx * 16;
-    for (int blk = 0; blk < 16; blk++) {
-        int ras = BLK2RAS[blk], ox = (ras & 3) * 4, oy = (ras >> 2) * 4;
-        IntraNb n4;
-        get_nb4(e->rec[0], e->cw, mbx, mby, e->mbw, ras, &n4);
-        int pm = i4_pred_mode(e->mbs, &t, e->mbw, mbx, mby, ras);
-        int best = -1, bc = 0, d[16];
-        uint8_t p[16], bp[16];
-        for (int m = 0; m < 9; m++) {
-            if (!pred4x4_avail(&n4, m)) continue;
-            pred4x4(&n4, m, p);
-            for (int y = 0; y < 4; y++) for (int x = 0; x < 4; x++) d[4 * y + x] = src[(oy + y) * e->cw + ox + x] - p[4 * y + x];
-            int c = satd4(d) + lam * (m == pm ? 1 : 4);
-            if (best < 0 || c < bc) { best = m; bc = c; memcpy(bp, p, 16); }
+    const int flags = mb_nb_flags(mbx, mby, e->mbw);
+    int won = 0;
+    if (h264o_vaa_intra_var(src, e->cw) > OH_VAA_I4_THRESHOLD) {
+        int sum = 0;
+        won = 1;
+        for (int blk = 0; blk < 16; blk++) {
+            int ras = BLK2RAS[blk], ox = (ras & 3) * 4, oy = (ras >> 2) * 4;
+            IntraNb n4;
+            get_nb4(e->rec[0], e->cw, mbx, mby, e->mbw, ras, &n4);
+            const int pm = i4_pred_mode(e->mbs, &t, e->mbw, mbx, mby, ras);
+            const int ai = OH_I4_AVAIL_IDX[flags][blk];
+            int c[9];
+            uint8_t p[16];
+            for (int m = 0; m < 9; m++) {
+                c[m] = 0x7fffffff;
+                if (!pred4x4_avail(&n4, m)) continue;
+                pred4x4(&n4, m, p);
+                c[m] = sad_blk(src + oy * e->cw + ox, e->cw, p, 4, 4, 4) + (m == pm ? lam : lam << OH_I4_MODE_BITS_SHIFT);
+            }
+            int bc;
+            const int best = h264o_i4_choose(c, ai, &bc);
+            sum += bc;
+            if (sum >= c16) { won = 0; break; }
+            pred4x4(&n4, best, p);
+            t.i4mode[ras] = (int8_t)best;
+            luma_block_levels(src + oy * e->cw + ox, e->cw, p, 4, mb->qp, 1, 0, t.luma[ras]);
+            int coef[16];
+            dequant_block(t.luma[ras], mb->qp, 0, coef);
+            idct4_add(coef, dst + oy * e->cw + ox, e->cw, p, 4);
+            t.nnz[ras] = (uint8_t)count_nz(t.luma[ras], 16);
         }
-        cost4 += bc;
-        if (cost4 >= c16) { won = 0; break; }
-        t.i4mode[ras] = (int8_t)best;
-        luma_block_levels(src + oy * e->cw + ox, e->cw, bp, 4, mb->qp, 1, 0, t.luma[ras]);
-        int coef[16];
-        dequant_block(t.luma[ras], mb->qp, 0, coef);
-        idct4_add(coef, dst + oy * e->cw + ox, e->cw, bp, 4);
-        t.nnz[ras] = (uint8_t)count_nz(t.luma[ras], 16);
+        if (won && sum + OH_I4_MB_OVERHEAD * lam >= c16) won = 0;
     }
     if (won) {
         *mb = t;

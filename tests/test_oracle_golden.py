@@ -295,3 +295,107 @@ def test_slice_headers_pinned(oracle):
         r.se()
         assert [r.ue(), r.se(), r.se()] == [0, 0, 0]
     assert idr_ids == [1, 2]
+
+
+def test_openh264_md_constants_pinned(oracle):
+    """The intra mode decision's constants the oracle applies are the immediates the fixture cites:
+    the VAA variance above which Intra4x4 is tried (func 774), the non-predicted mode's lambda shift and the
+    Intra4x4 MB overhead (x lambda); and the camera / low-complexity path installs that function and SAD costs
+    (func 1017: table entry 254, pfSampleSad at function-list offset 84)."""
+    c = OH['code_constants']
+    out = (ctypes.c_int32 * 3)()
+    oracle.L.h264o_md_constants(out)
+    assert list(out) == [c['md_vaa_i4_threshold']['value'], c['md_i4_mode_bits_shift']['value'], c['md_i4_mb_overhead']['value']]
+    assert c['md_camera_intra_fine_md']['value'] == 254 and c['md_camera_md_cost_array']['value'] == 84
+
+
+def test_vaa_intra_var_restatement(oracle):
+    """AnalysisVaaInfoIntra (h264.wasm func 854) restated in numpy: the sixteen 4x4 means (sum >> 4), then
+    sum of squares - (sum^2 >> 4), on random and flat MBs"""
+    rng = np.random.default_rng(3)
+    oracle.L.h264o_vaa_intra_var.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    for k in range(200):
+        mb = rng.integers(0, 256, (16, 16), dtype=np.uint8) if k % 3 else np.full((16, 16), k, np.uint8)
+        if k % 5 == 0:
+            mb = (mb // 32).astype(np.uint8) + 100
+        m = mb.reshape(4, 4, 4, 4).sum(axis=(1, 3)).astype(np.int64) >> 4
+        want = int((m * m).sum() - ((int(m.sum()) ** 2) >> 4))
+        buf = np.ascontiguousarray(mb)
+        assert oracle.L.h264o_vaa_intra_var(buf.ctypes.data, 16) == want
+
+
+def _i4_choose_listing(c, ai, t):
+    """WelsMdI4x4Fast's per-block choice written from the listing of h264.wasm func 774 (475330-476768), its
+    locals kept: L2 best cost, L4 mode, L6 / L10 / L14 / L17 the costs it compares; c = cost per syntax mode"""
+    cnt = t['i4_avail_count']['values'][ai]
+    if cnt == 0:
+        return 0, 0x7fffffff
+    if cnt not in (7, 9):
+        best, mode = 0x7fffffff, 0
+        for im in t['i4_avail_modes']['values'][ai][:cnt]:
+            m = t['i4_mode_map']['values'][im]
+            if best > c[m]:
+                best, mode = c[m], m
+        return mode, best
+    L2 = c[2]                        # DC
+    L10 = c[1]                       # H
+    L0 = L2
+    lt = L10 < L0
+    L6 = c[0]                        # V
+    L17 = L10 if lt else L0
+    L14 = L6 < L17
+    L4 = 0 if L14 else (1 if lt else 2)
+    L2 = L6 if L14 else L17
+    if L6 < L10:
+        if cnt == 9:
+            L14 = c[5]; L3 = L14 < L2
+            L17 = c[7]
+            L2 = L14 if L3 else L2
+            L10b = L2 > L17
+            L2 = L17 if L10b else L2
+            L4 = 7 if L10b else (5 if L3 else L4)
+            if L6 <= L17 and L6 <= L14:
+                return L4, L2
+            if L14 < L17:
+                L8 = c[4]
+                return (L4, L2) if L8 >= L2 else (4, L8)
+            L8 = c[3]
+            return (L4, L2) if L8 >= L2 else (3, L8)
+        L6b = c[4]; L9 = L6b < L2
+        L8 = c[5]
+        L2 = L6b if L9 else L2
+        if L8 >= L2:
+            return (4 if L9 else L4), L2
+        return 5, L8
+    L9 = c[6]; L17b = L9 < L2
+    L6 = c[8]
+    L2 = L9 if L17b else L2
+    L20 = L2 > L6
+    L2 = L6 if L20 else L2
+    L4 = 8 if L20 else (6 if L17b else L4)
+    if L9 >= L10 and L6 >= L10:
+        return L4, L2
+    if L6 > L9:
+        L8 = c[4]
+        return (L4, L2) if L8 >= L2 else (4, L8)
+    if cnt != 9:
+        return L4, L2
+    L8 = c[3]
+    return (L4, L2) if L8 >= L2 else (3, L8)
+
+
+def test_i4_choose_vs_listing(oracle):
+    """the oracle's Intra4x4 block choice (h264o_i4_choose) == the listing-shaped Python restatement above over
+    random cost vectors with many ties, for every availability index"""
+    t = OH['tables']
+    rng = np.random.default_rng(11)
+    oracle.L.h264o_i4_choose.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    cost = ctypes.c_int32()
+    for k in range(6000):
+        ai = k % 16
+        c = (rng.integers(0, 12, 9) * (4 if k % 2 else 1)).astype(np.int32)
+        got = oracle.L.h264o_i4_choose(c.ctypes.data, ai, ctypes.byref(cost))
+        if t['i4_avail_count']['values'][ai] == 0:
+            continue
+        want = _i4_choose_listing([int(x) for x in c], ai, t)
+        assert (got, cost.value) == want, (ai, c.tolist())

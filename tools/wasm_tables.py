@@ -158,6 +158,20 @@ TABLES = {
                      'one temporal layer -> row 0, weight 2000 = WEIGHT_MULTIPLY'),
     'logf_table': (73408, 'd', (16, 2), 'musl logf {invc, logc}[16] (func 483, called by RcConvertQStep2Qp in func 1226)'),
     'logf_poly': (73664, 'd', (4,), 'musl logf {Ln2, A[0], A[1], A[2]} (func 483)'),
+    # intra mode decision at the wrapper's settings (camera usage, complexity LOW: DESIGN.md §3.3)
+    'i16_avail_modes': (42624, 'b', (8, 5), 'g_kiIntra16AvaliMode[neighbour flags & 7]: the I16x16 modes WelsMdI16x16 (func 313) '
+                        'tries, in order (0 V, 1 H, 2 DC, 3 P, 4 DC_L, 5 DC_T, 6 DC_128), count in column 4'),
+    'i16_mode_map': (40976, 'b', (7,), 'g_kiMapModeI16x16: the syntax mode (Intra16x16PredMode) of each internal mode'),
+    'chroma_avail_modes': (42992, 'b', (8, 5), 'g_kiIntraChromaAvailMode[neighbour flags & 7]: the chroma modes '
+                           'WelsMdIntraChroma (func 312) tries, in order (0 DC, 1 H, 2 V, 3 P, 4 DC_L, 5 DC_T, 6 DC_128)'),
+    'chroma_mode_map': (40983, 'b', (7,), 'g_kiMapModeIntraChroma: the syntax mode (intra_chroma_pred_mode) of each internal mode'),
+    'i4_avail_index': (42688, 'b', (16, 16), 'g_kiNeighborIntraToI4x4[MB neighbour flags: 1 left, 2 top, 4 top-left, 8 '
+                       'top-right][4x4 block, decoding order]: the block\'s availability index (same bits)'),
+    'i4_avail_count': (42672, 'b', (16,), 'g_kiIntra4AvailCount[availability index]: modes WelsMdI4x4Fast (in func 774) tries; '
+                       '7 and 9 take its fast search'),
+    'i4_avail_modes': (43120, 'b', (16, 16), 'g_kiIntra4AvailMode[availability index]: the Intra4x4 modes in order '
+                       '(0..8 the standard\'s, 9 DC_L, 10 DC_T, 11 DC_128)'),
+    'i4_mode_map': (42976, 'b', (16,), 'g_kiMapModeI4x4: the syntax mode (Intra4x4PredMode) of each internal mode'),
     'level_limits': (63120, 'i', (17, 8), 'g_ksLevelLimits {level_idc, MaxMBPS, MaxFS, MaxDpbMbs, MaxBR, MaxCPB, MinVmv, MaxVmv} '
                      '(WelsInitSps, func 280, walks it in this order)'),
 }
@@ -211,6 +225,16 @@ CODE_CONSTANTS = {
     'gom_ratio_up1': (759608, 'i64.const', 1215, 'RcCalculateGomQp: QP + 1 below this ratio'),
     'gom_ratio_down1': (759623, 'i64.const', 1215, 'RcCalculateGomQp: QP - 1 above this ratio'),
     'gom_var_sample_shift': (530814, 'i32.const', 910, 'AnalyzeGomComplexityViaVar: sample count = first-row MBs << this'),
+    # intra mode decision (oracle encode_intra_mb / best_chroma_mode; GPU enc_mb_kernel.inc)
+    'md_camera_intra_fine_md': (675919, 'i32.const', 1017, 'PreprocessSliceCoding: pfIntraFineMd = table entry 254 '
+                                '(func 774, WelsMdIntraFinePartitionVaa) for camera usage with iComplexityMode (param '
+                                '+832) 0 -- the wrapper\'s'),
+    'md_camera_md_cost_array': (675952, 'i32.const', 1017, 'PreprocessSliceCoding: pfMdCost = the function list + this '
+                                '(pfSampleSad; + 112 is pfSampleSatd, the other branch): mode costs are SADs'),
+    'md_vaa_i4_threshold': (474996, 'i32.const', 774, 'WelsMdIntraFinePartitionVaa: Intra4x4 is tried only when the source '
+                            'MB\'s 4x4-mean variance (func 854) is above this'),
+    'md_i4_mode_bits_shift': (475108, 'i32.const', 774, 'WelsMdI4x4Fast: a mode other than the predicted one costs lambda << this'),
+    'md_i4_mb_overhead': (476981, 'i32.const', 774, 'WelsMdI4x4Fast: the I4x4 MB costs its blocks + lambda * this'),
     # stream syntax (oracle h264o_write_sps / h264o_enc_encode)
     'sps_log2_max_frame_num_and_poc_type': (167923, 'i64.const', 280, 'WelsInitSps: one i64 store of '
                                             '{uiLog2MaxFrameNum (low word), uiPocType (high word)}'),
@@ -261,7 +285,7 @@ def extract(path):
         vals, fo = mem.read(addr, fmt, n)
         if len(shape) == 2:
             vals = [vals[r * shape[1]:(r + 1) * shape[1]] for r in range(shape[0])]
-        out['tables'][name] = {'address': addr, 'file_offset': fo, 'type': {'h': 'int16', 'i': 'int32', 'd': 'f64'}[fmt],
+        out['tables'][name] = {'address': addr, 'file_offset': fo, 'type': {'b': 'int8', 'B': 'uint8', 'h': 'int16', 'i': 'int32', 'd': 'f64'}[fmt],
                                'shape': list(shape), 'meaning': meaning, 'values': vals}
     for name, (off, op, func, meaning) in CODE_CONSTANTS.items():
         out['code_constants'][name] = {'file_offset': off, 'instruction': op.replace('f32bits', 'i32.const (f32 bits)'),
