@@ -116,9 +116,8 @@ def test_rc_row_plan(oracle):
 
 def test_frame_skip_and_row_qp_in_stream(oracle):
     """at a bitrate far below the content's cost, non-IDR frames are skipped (0 bytes) while the
-    virtual buffer holds more than half a second of bits; coded P frames carry mb_qp_delta != 0
-    (per-row QPs) and still decode to the encoder's reconstruction; with skipping off every frame
-    is coded"""
+    virtual buffer holds more than half a second of bits; with skipping off every frame is coded; the coded P
+    frames carry mb_qp_delta != 0 (per-row QPs) and decode to the encoder's reconstruction"""
     from h264mi.synth import SyntheticStream
     w, h = 352, 288
     g = SyntheticStream(2, w, h)
@@ -135,10 +134,17 @@ def test_frame_skip_and_row_qp_in_stream(oracle):
             oracle.L.h264o_dec_mbinfo(od.d, mi.ctypes.data)
             qps_seen |= set(mi.reshape(-1, 8)[:, 1].tolist())
     assert sizes[0] > 0 and 0 in sizes and oracle.L.h264o_enc_frames_skipped(oe.e) == sizes.count(0)
-    assert len(qps_seen) > 1, qps_seen   # more than one QPY within pictures: mb_qp_delta was coded
-    oe2 = oracle.encoder(w, h, 200000)
+    oe2, od2 = oracle.encoder(w, h, 200000), oracle.decoder()
     oracle.L.h264o_enc_set_frame_skip(oe2.e, 0)
-    assert all(len(oe2.encode(f)) > 0 for f in frames)
+    for f in frames:
+        nal = oe2.encode(f)
+        assert len(nal) > 0
+        rc, pic, _, _ = od2.decode(nal)
+        assert rc == 1 and np.array_equal(pic, oe2.recon())
+        mi = np.zeros((w // 16) * (h // 16) * 8, np.int32)
+        oracle.L.h264o_dec_mbinfo(od2.d, mi.ctypes.data)
+        qps_seen |= set(mi.reshape(-1, 8)[:, 1].tolist())
+    assert len(qps_seen) > 1, qps_seen   # more than one QPY within pictures: mb_qp_delta was coded
 
 
 def test_motion_search_stages_exercised(oracle):
