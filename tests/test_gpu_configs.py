@@ -282,3 +282,38 @@ def test_stream_grouped_tickets_same_bytes(gpu_lib, sgrp):
         outs.append(got)
         enc.close()
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize('w,h', [(16, 16), (48, 16), (16, 48), (32, 32), (80, 48), (176, 144)])
+def test_intra_decision_geometries_vs_oracle(gpu_lib, oracle, w, h):
+    """OpenH264's intra mode decision (the I16x16 / chroma mode orders by neighbour flags, the
+    VAA gate, WelsMdI4x4Fast's fast and table paths by block availability) at picture edges: one-MB-wide and
+    one-MB-high pictures (no top-right, no left or no top anywhere), every frame an IDR, content from flat to
+    noise (VAA variance below and above 149) at two rates; GPU bytes == oracle bytes"""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    rng = np.random.default_rng(w * 131 + h)
+    fs = w * h * 3 // 2
+    g = SyntheticStream(9, w, h)
+    clips = []
+    for t in range(4):
+        flat = np.full(fs, 90 + 7 * t, np.uint8)
+        noise = rng.integers(0, 256, fs, dtype=np.uint8)
+        tex = np.ascontiguousarray(g.frame(t))
+        clips.append(np.stack([flat if t == 0 else tex, noise]))
+    for br in (300000, 4000000):
+        enc = h264mi.BatchEncoder(w, h, br, 2)
+        enc.set_frame_skip(False)
+        oes = [oracle.encoder(w, h, br) for _ in range(2)]
+        for oe in oes:
+            oe.set_frame_skip(False)
+        for t in range(4):
+            enc.force_idr(-1)
+            enc.encode(torch.from_numpy(clips[t]).cuda())
+            n = enc.nal_sizes()
+            for s in range(2):
+                oes[s].force_idr()
+                ref = oes[s].encode(clips[t][s])
+                assert n[s] == len(ref) and enc.nal_bytes(s, n[s]) == ref, (br, t, s)
+        enc.close()
