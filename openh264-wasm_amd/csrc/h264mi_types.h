@@ -127,6 +127,10 @@ struct EncDesc {
     uint32_t *gomc;         // per GOM: [0, G) SAD against the last coded source (P), [G, 2G) variance (I)
     uint64_t *bitg;         // exact GOM mode: per MB {epoch, macroblock_layer() bits} granules (the CAVLC waves)
     uint64_t *gomst;        // exact GOM mode: per GOM 4 granules {QP, slice bits before it, target bits, last coded MB + 1}
+    // the P_Skip judge's memory: per MB the skip SAD of a skipped MB, -1 for any other, then one word
+    // "the picture is P"; the reference picture's (last coded frame) and this frame's (swapped with ref / dbk)
+    const int32_t *sksad_ref;
+    int32_t *sksad_cur;
 };
 
 // One stream's padded reference planes and the picture they are built from (enc_planes.inc).

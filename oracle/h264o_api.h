@@ -32,7 +32,12 @@ void h264o_enc_set_frame_skip(H264OEnc *e, int enable);
 int h264o_enc_frames_skipped(const H264OEnc *e);
 /* motion-search stage counters since creation: cross searches run, cross searches that moved the
  * vector, start points won by a neighbour candidate (A, B or C) */
-void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]);
+/* {cross searches, cross searches that moved, neighbour start points won, P_Skip judges run, double-check skips} */
+void h264o_enc_me_stats(const H264OEnc *e, int32_t out[5]);
+/* WelsCalculateSingleCtr4x4 (h264.wasm func 1011) over 16 levels in scan order */
+int h264o_single_ctr(const int16_t lv[16]);
+/* {mv min, mv max low bits, max level, luma single-ctr max, chroma single-ctr max} */
+void h264o_pskip_constants(int32_t out[5]);
 int h264o_rc_row_delta(int64_t row_bits, int64_t mean);
 int h264o_rc_init_qp(int w, int h, int bitrate);
 int h264o_rc_idr_params(int w, int h, int bitrate, int *rmin, int *rmax);  /* first IDR QP, IDR QP range */

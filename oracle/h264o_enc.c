@@ -32,6 +32,12 @@
 #define OH_VAA_I4_THRESHOLD 149  /* WelsMdIntraFinePartitionVaa: I4x4 tried when the VAA variance is above this */
 #define OH_I4_MODE_BITS_SHIFT 2  /* a mode other than the predicted one costs lambda << 2 */
 #define OH_I4_MB_OVERHEAD 24     /* the I4x4 MB costs its blocks + 24 lambda */
+/* P_Skip judge (CODE_CONSTANTS pskip_*, TABLES single_ctr_run) */
+#define OH_PSKIP_MV_MIN (-29)        /* WelsMdPSkipEnc: (mv >> 2) + 16 * MB position below this: no skip */
+#define OH_PSKIP_MV_MAX_LOW 12       /* ... or above (16 * MBs) | this */
+#define OH_PSKIP_MAX_LEVEL 1         /* a 4x4 block with a larger |level| rejects the skip */
+#define OH_PSKIP_LUMA_CTR_MAX 5      /* the MB's summed single-coefficient cost of luma blocks: at most this */
+#define OH_PSKIP_CHROMA_CTR_MAX 6    /* a chroma plane's: at most this */
 /* Stream syntax OpenH264 writes at the wrapper's parameters, read from the same binary's code
  * (tools/wasm_tables.py CODE_CONSTANTS pins each instruction): WelsInitSps (func 280) stores
  * uiLog2MaxFrameNum 15 and uiPocType 2 as one i64 constant (sps_log2_max_frame_num_and_poc_type, 167923), so the slice header
@@ -109,7 +115,10 @@ struct H264OEnc {
     int *rowqp;       /* QP offset plan of the next frame, one per MB row (added to the frame QP) */
     int64_t *rowbits; /* macroblock_layer() bits per MB row of the last coded frame */
     int skipped, last_skipped;
-    int stat_cross, stat_cross_moved, stat_nb_start;  /* ME path counters (tests: coverage of the search stages) */
+    /* per MB, the P_Skip judge's memory (func 734): the skip SAD (luma + chroma SAD of the prediction at the skip
+     * vector) of a skipped MB, -1 for any other; this frame's and the reference picture's (last coded frame) */
+    int32_t *sksad_cur, *sksad_ref;
+    int stat_cross, stat_cross_moved, stat_nb_start, stat_skip_tried, stat_skip_double;  /* ME path counters (tests: coverage of the search stages) */
 };
 
 /* ---------------- rate control ---------------- */
@@ -451,6 +460,11 @@ static void rc_plan_rows(H264OEnc *e) {
 }
 /* the intra mode decision's constants for tests/test_oracle_golden.py: {VAA threshold, mode bits shift, I4x4 MB
  * overhead} (pinned against the h264.wasm fixture, tools/wasm_tables.py md_*) */
+/* the P_Skip judge's constants (tests check them against the binary's instructions) */
+void h264o_pskip_constants(int32_t out[5]) {
+    out[0] = OH_PSKIP_MV_MIN; out[1] = OH_PSKIP_MV_MAX_LOW; out[2] = OH_PSKIP_MAX_LEVEL;
+    out[3] = OH_PSKIP_LUMA_CTR_MAX; out[4] = OH_PSKIP_CHROMA_CTR_MAX;
+}
 void h264o_md_constants(int32_t out[3]) {
     out[0] = OH_VAA_I4_THRESHOLD; out[1] = OH_I4_MODE_BITS_SHIFT; out[2] = OH_I4_MB_OVERHEAD;
 }
@@ -481,6 +495,8 @@ int h264o_table(const char *name, double *out) {
     else if (!strcmp(name, "i4_avail_modes")) { for (int i = 0; i < 256; i++) out[n++] = OH_I4_MODES[i / 16][i % 16]; }
     else if (!strcmp(name, "i4_mode_map")) { for (int i = 0; i < 16; i++) out[n++] = OH_I4_MAP[i]; }
     else if (!strcmp(name, "level_limits")) { for (int i = 0; i < 17 * 6; i++) out[n++] = OH_LEVEL_LIMITS[i / 6][i % 6]; }
+    else if (!strcmp(name, "single_ctr_run")) { for (int i = 0; i < 16; i++) out[n++] = OH_SINGLE_CTR[i]; }
+    else if (!strcmp(name, "chroma_qp")) { for (int i = 0; i < 52; i++) out[n++] = CHROMA_QP[i]; }
     else return -1;
     return n;
 }
@@ -928,6 +944,101 @@ static int inter_levels(H264OEnc *e, MBInfo *mb, int mbx, int mby, const uint8_t
     if (mb->cbp >> 4) any = 1;
     return any;
 }
+/* ---------------- OpenH264's P_Skip judge ---------------- */
+/* WelsCalculateSingleCtr4x4 (func 1011): from the last non-zero level down (scan order), each non-zero level adds
+ * OH_SINGLE_CTR[the run of zeros below it, to the next non-zero level or to the start] */
+int h264o_single_ctr(const int16_t lv[16]) {
+    int k = 15, s = 0;
+    while (k >= 0 && lv[k] == 0) k--;
+    while (k >= 0) {
+        int j = k - 1;
+        while (j >= 0 && lv[j] == 0) j--;
+        s += OH_SINGLE_CTR[k - 1 - j];
+        k = j;
+    }
+    return s;
+}
+/* WelsMdPSkipEnc's residual test (func 415 235160-235655, WelsTryPUVskip func 534): the luma 4x4 blocks of the MB
+ * predicted at the skip vector quantised at the MB's QP (inter rounding, every position; pfQuantizationFour4x4Max,
+ * func 1060): a block with a level above 1 rejects, and the single-coefficient costs of the blocks with a level
+ * of 1 may sum to at most 5 over the MB; per chroma plane, at the chroma QP: a non-zero quantised 2x2 DC
+ * coefficient rejects (pfQuantizationHadamard2x2Skip, func 1050), then each block quantised at every position (its
+ * DC coefficient by the AC rule too) may have no level above 1, and the single-coefficient costs of the AC levels
+ * (pfScan4x4Ac, func 1012) may sum to at most 6 per plane. Returns 1 when the residual admits the skip. */
+static int pskip_residual_ok(H264OEnc *e, int mbx, int mby, int qp, const uint8_t pl[256], uint8_t pc[2][64]) {
+    const uint8_t *src = e->src[0] + mby * 16 * e->cw + mbx * 16;
+    int ctr = 0;
+    for (int ras = 0; ras < 16; ras++) {
+        const int ox = (ras & 3) * 4, oy = (ras >> 2) * 4;
+        int d[16], c[16], mx = 0;
+        int16_t lv[16];
+        for (int y = 0; y < 4; y++) for (int x = 0; x < 4; x++) d[4 * y + x] = src[(oy + y) * e->cw + ox + x] - pl[(oy + y) * 16 + ox + x];
+        fdct4(d, c);
+        for (int k = 0; k < 16; k++) { lv[k] = (int16_t)quant4(c[ZIGZAG4[k]], qp, ZIGZAG4[k], 0); mx = imax(mx, iabs(lv[k])); }
+        if (mx > OH_PSKIP_MAX_LEVEL) return 0;
+        if (mx == 1) ctr += h264o_single_ctr(lv);
+        if (ctr > OH_PSKIP_LUMA_CTR_MAX) return 0;
+    }
+    const int qpc = CHROMA_QP[qp], cs = e->cw / 2;
+    for (int p = 0; p < 2; p++) {
+        const uint8_t *cs_src = e->src[1 + p] + mby * 8 * cs + mbx * 8;
+        int c4[4][16];
+        for (int blk = 0; blk < 4; blk++) {
+            const int ox = (blk & 1) * 4, oy = (blk >> 1) * 4;
+            int d[16];
+            for (int y = 0; y < 4; y++) for (int x = 0; x < 4; x++) d[4 * y + x] = cs_src[(oy + y) * cs + ox + x] - pc[p][(oy + y) * 8 + ox + x];
+            fdct4(d, c4[blk]);
+        }
+        const int a = c4[0][0], b = c4[1][0], cc = c4[2][0], dd = c4[3][0];
+        if (quant_dc4(a + b + cc + dd, qpc, 0) || quant_dc4(a - b + cc - dd, qpc, 0) || quant_dc4(a + b - cc - dd, qpc, 0) ||
+            quant_dc4(a - b - cc + dd, qpc, 0))
+            return 0;
+        int pctr = 0;
+        for (int blk = 0; blk < 4; blk++) {
+            int16_t lv[16], ac[16];
+            int mx = 0;
+            for (int k = 0; k < 16; k++) { lv[k] = (int16_t)quant4(c4[blk][ZIGZAG4[k]], qpc, ZIGZAG4[k], 0); mx = imax(mx, iabs(lv[k])); }
+            if (mx > OH_PSKIP_MAX_LEVEL) return 0;
+            if (mx == 1) {
+                for (int k = 0; k < 15; k++) ac[k] = lv[k + 1];
+                ac[15] = 0;
+                pctr += h264o_single_ctr(ac);
+                if (pctr > OH_PSKIP_CHROMA_CTR_MAX) return 0;
+            }
+        }
+    }
+    return 1;
+}
+/* PredictSadSkip (func 331): the skip SAD the neighbours predict -- A left, B top, C top-right (top-left when the
+ * top-right MB is outside the picture); a neighbour counts with its skip SAD if it was skipped, else 0. One skipped
+ * neighbour: its SAD; otherwise the median of the three. Without a top or top-left MB: the left MB's. */
+static int predict_sad_skip(const H264OEnc *e, int mbx, int mby) {
+    const int mbw = e->mbw, n = mby * mbw + mbx;
+    const int avA = mbx > 0, avB = mby > 0, avC = mby > 0 && mbx + 1 < mbw, avD = mbx > 0 && mby > 0;
+#define SK(av, i) ((av) && e->mbs[i].type == MBT_PSKIP)
+    const int skA = SK(avA, n - 1), skB = SK(avB, n - mbw);
+    int skC = SK(avC, n - mbw + 1);
+    const int sA = skA ? e->sksad_cur[n - 1] : 0, sB = skB ? e->sksad_cur[n - mbw] : 0;
+    int sC = skC ? e->sksad_cur[n - mbw + 1] : 0, avCC = avC;
+    if (!avC) {
+        skC = SK(avD, n - mbw - 1);
+        sC = skC ? e->sksad_cur[n - mbw - 1] : 0;
+        avCC = avD;
+        if (!avB && !avCC && avA) return sA;
+    }
+#undef SK
+    switch (skA | (skB << 1) | (skC << 2)) {
+    case 1: return sA;
+    case 2: return sB;
+    case 4: return sC;
+    default: return sA + sB + sC - imin(sA, imin(sB, sC)) - imax(sA, imax(sB, sC));
+    }
+}
+static int sad_mb_pred(H264OEnc *e, int mbx, int mby, const uint8_t pl[256], uint8_t pc[2][64]) {
+    const int cs = e->cw / 2;
+    return sad_blk(e->src[0] + mby * 16 * e->cw + mbx * 16, e->cw, pl, 16, 16, 16) +
+           sad_blk(e->src[1] + mby * 8 * cs + mbx * 8, cs, pc[0], 8, 8, 8) + sad_blk(e->src[2] + mby * 8 * cs + mbx * 8, cs, pc[1], 8, 8, 8);
+}
 static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
     int lam = LAMBDA[mb->qp];
     Pic rp = {e->ref[0], e->ref[1], e->ref[2], e->cw, e->ch, e->cw, e->cw / 2};
@@ -936,19 +1047,39 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
     int skmv[2], mvp[2];
     pskip_mv(e->mbs, e->mbw, mbx, mby, skmv);
     mvp_16x16(e->mbs, e->mbw, mbx, mby, mvp);
-    /* 1. P_Skip test: skip iff every quantised level at the skip MV is zero */
-    mc_luma(&rp, mbx * 16, mby * 16, 16, 16, skmv[0], skmv[1], pl, 16);
-    mc_chroma(e->ref[1], cs, e->ch / 2, cs, mbx * 8, mby * 8, 8, 8, skmv[0], skmv[1], pc[0], 8);
-    mc_chroma(e->ref[2], cs, e->ch / 2, cs, mbx * 8, mby * 8, 8, 8, skmv[0], skmv[1], pc[1], 8);
-    MBInfo t = *mb;
-    if (!inter_levels(e, &t, mbx, mby, pl, pc)) {
+    /* 1. OpenH264's P_Skip judge (WelsMdInterMb func 746, WelsMdPSkipEnc func 415): tried when a
+     * neighbour (left, top, top-left, top-right) was skipped, or, on a P reference picture, the co-located MB was;
+     * then, unless the skip vector points too far outside the picture, the skip is taken when the prediction's SAD
+     * (luma + chroma) is 0, below the neighbours' predicted skip SAD, or (P reference, co-located MB skipped) below
+     * that MB's skip SAD -- else when its residual passes pskip_residual_ok. (OpenH264 then tries the intra modes
+     * unless the left, top and top-right MBs were all skipped; here a taken skip is final: own.) */
+    const int n = mby * e->mbw + mbx, mbw = e->mbw;
+    const int ref_p = !e->last_idr, ref_skip = ref_p && e->sksad_ref[n] >= 0;
+    const int try_skip = (mbx > 0 && e->mbs[n - 1].type == MBT_PSKIP) || (mby > 0 && e->mbs[n - mbw].type == MBT_PSKIP) ||
+                         (mbx > 0 && mby > 0 && e->mbs[n - mbw - 1].type == MBT_PSKIP) ||
+                         (mby > 0 && mbx + 1 < mbw && e->mbs[n - mbw + 1].type == MBT_PSKIP) || ref_skip;
+    const int sx = (skmv[0] >> 2) + 16 * mbx, sy = (skmv[1] >> 2) + 16 * mby;
+    e->sksad_cur[n] = -1;
+    if (try_skip && sx >= OH_PSKIP_MV_MIN && sx <= ((16 * mbw) | OH_PSKIP_MV_MAX_LOW) && sy >= OH_PSKIP_MV_MIN &&
+        sy <= ((16 * e->mbh) | OH_PSKIP_MV_MAX_LOW)) {
+        mc_luma(&rp, mbx * 16, mby * 16, 16, 16, skmv[0], skmv[1], pl, 16);
+        mc_chroma(e->ref[1], cs, e->ch / 2, cs, mbx * 8, mby * 8, 8, 8, skmv[0], skmv[1], pc[0], 8);
+        mc_chroma(e->ref[2], cs, e->ch / 2, cs, mbx * 8, mby * 8, 8, 8, skmv[0], skmv[1], pc[1], 8);
+        const int tsad = sad_mb_pred(e, mbx, mby, pl, pc);
+        const int take = tsad == 0 || tsad < predict_sad_skip(e, mbx, mby) || (ref_skip && tsad < e->sksad_ref[n]) ||
+                         pskip_residual_ok(e, mbx, mby, mb->qp, pl, pc);
+        e->stat_skip_tried++;
+        if (take) e->sksad_cur[n] = tsad;
+    }
+    if (e->sksad_cur[n] >= 0) {  /* P_Skip: the reconstruction is the prediction */
+        for (int p = 0; p < 2; p++)
+            for (int y = 0; y < 8; y++) memcpy(e->rec[1 + p] + (mby * 8 + y) * cs + mbx * 8, pc[p] + 8 * y, 8);
         mb->type = MBT_PSKIP; mb->cbp = 0;
         memset(mb->nnz, 0, sizeof(mb->nnz));
         for (int i = 0; i < 16; i++) { mb->mv[i][0] = (int16_t)skmv[0]; mb->mv[i][1] = (int16_t)skmv[1]; mb->i4mode[i] = 2; }
         for (int i = 0; i < 4; i++) mb->ref[i] = 0;
         uint8_t *dst = e->rec[0] + mby * 16 * e->cw + mbx * 16;
         for (int y = 0; y < 16; y++) memcpy(dst + y * e->cw, pl + 16 * y, 16);
-        /* chroma already reconstructed with zero residual == prediction */
         return;
     }
     /* 2. integer ME: start candidates {mvp, (0,0), A, B, C} (the MV predictors'
@@ -1038,6 +1169,13 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
         dequant_block(mb->luma[ras], mb->qp, 0, coef);
         idct4_add(coef, dst + oy * e->cw + ox, e->cw, pl + oy * 16 + ox, 16);
     }
+    /* 6. WelsMdInterDoubleCheckPskip (func 399 217892-217961): a P16x16 MB with no coded residual at the skip vector
+     * is a P_Skip (same reconstruction); its skip SAD for the judge is the prediction's SAD there */
+    if (mb->cbp == 0 && mx == skmv[0] && my == skmv[1]) {
+        mb->type = MBT_PSKIP;
+        e->sksad_cur[n] = sad_mb_pred(e, mbx, mby, pl, pc);
+        e->stat_skip_double++;
+    }
 }
 
 /* ---------------- macroblock_layer() writer (7.3.5) ---------------- */
@@ -1116,6 +1254,9 @@ H264OEnc *h264o_enc_create(int w, int h, int bitrate) {
     e->rowqp = (int *)calloc((size_t)e->mbh, sizeof(int));
     e->rowbits = (int64_t *)calloc((size_t)e->mbh, sizeof(int64_t));
     e->prev_src = (uint8_t *)calloc((size_t)e->cw * e->ch, 1);
+    e->sksad_cur = (int32_t *)malloc((size_t)e->mbw * e->mbh * sizeof(int32_t));
+    e->sksad_ref = (int32_t *)malloc((size_t)e->mbw * e->mbh * sizeof(int32_t));
+    for (int i = 0; i < e->mbw * e->mbh; i++) e->sksad_cur[i] = e->sksad_ref[i] = -1;
     e->rc.gom_sad = (uint32_t *)calloc((size_t)e->mbw * e->mbh, sizeof(uint32_t));
     e->rc.gom_trace = (int32_t *)calloc(4 * (size_t)e->mbw * e->mbh, sizeof(int32_t));
     rc_init(&e->rc, w, h, bitrate);  /* frame skipping on: the wrapper leaves bEnableFrameSkip at its default */
@@ -1127,7 +1268,7 @@ void h264o_enc_destroy(H264OEnc *e) {
     if (!e) return;
     for (int p = 0; p < 3; p++) { free(e->src[p]); free(e->rec[p]); free(e->ref[p]); }
     free(e->prev_src); free(e->rc.gom_sad); free(e->rc.gom_trace);
-    free(e->mbs); free(e->rowqp); free(e->rowbits); free(e);
+    free(e->mbs); free(e->rowqp); free(e->rowbits); free(e->sksad_cur); free(e->sksad_ref); free(e);
 }
 /* bEnableFrameSkip (on by default, as the wrapper leaves it): off, no frame is skipped, the VBV check is not
  * made, and an exhausted VGOP budget raises the QP instead (BITS_EXCEEDED) */
@@ -1152,8 +1293,9 @@ int h264o_enc_gom_state(const H264OEnc *e, int32_t *out, int cap) {
     return G;
 }
 int h264o_enc_frames_skipped(const H264OEnc *e) { return e ? e->skipped : 0; }
-void h264o_enc_me_stats(const H264OEnc *e, int32_t out[3]) {
+void h264o_enc_me_stats(const H264OEnc *e, int32_t out[5]) {
     out[0] = e->stat_cross; out[1] = e->stat_cross_moved; out[2] = e->stat_nb_start;
+    out[3] = e->stat_skip_tried; out[4] = e->stat_skip_double;
 }
 void h264o_enc_force_idr(H264OEnc *e) { if (e) e->force_idr = 1; }
 int h264o_enc_last_qp(const H264OEnc *e) { return e->last_qp; }
@@ -1254,6 +1396,7 @@ int h264o_enc_encode(H264OEnc *e, const uint8_t *yuv, uint8_t *out, int cap) {
     const size_t o_slice = o;
     o += nal_write(tmp + o, 3, idr ? 5 : 1, b.buf, b.len);
     bw_free(&b);
+    { int32_t *t = e->sksad_ref; e->sksad_ref = e->sksad_cur; e->sksad_cur = t; }
     /* loop filter on the reconstruction -> next reference */
     deblock_frame(e->rec[0], e->rec[1], e->rec[2], e->cw, e->cw / 2, e->mbs, e->mbw, e->mbh, 0);
     for (int p = 0; p < 3; p++) { uint8_t *t = e->ref[p]; e->ref[p] = e->rec[p]; e->rec[p] = t; }

@@ -66,7 +66,7 @@ def test_config3_1080p_ippp_8mbps_60_frames(gpu_lib, oracle):
     sizes, qps = _run_capi(gpu_lib, oracle, 1920, 1080, 8000000, 60, False)
     # the IDR (~490 KB at QP 30) fills the skip buffer (bitrate / 2, drained bitrate / 60 per frame): the
     # rate control drops some P frames after it, then codes the rest (GPU == oracle, skips included)
-    assert sum(1 for n in sizes[1:] if n > 0) >= 15, sizes  # P frames really coded
+    assert sum(1 for n in sizes[1:] if n > 0) >= 10, sizes  # P frames really coded
     assert qps[0] == 30 and max(qps) <= 42, qps
 
 

@@ -149,16 +149,17 @@ def test_frame_skip_and_row_qp_in_stream(oracle):
 
 def test_motion_search_stages_exercised(oracle):
     """the fixture workloads reach every integer-search stage the GPU is held bit-exact on: start
-    points won by a neighbour's vector, cross searches, and cross searches that move the vector"""
+    points won by a neighbour's vector, cross searches, and cross searches that move the vector; and both
+    ways an MB becomes P_Skip (the judge run, the double check after P16x16 coding)"""
     from h264mi.synth import SyntheticStream
-    tot = np.zeros(3, np.int64)
+    tot = np.zeros(5, np.int64)
     for sid, (w, h, br) in enumerate([(352, 288, 2000000), (640, 360, 1000000), (352, 288, 30000000)]):
         g = SyntheticStream(sid, w, h)
         oe = oracle.encoder(w, h, br)
         oe.set_frame_skip(False)
         for t in range(5):
             oe.encode(np.ascontiguousarray(g.frame(t)))
-        st = np.zeros(3, np.int32)
+        st = np.zeros(5, np.int32)
         oracle.L.h264o_enc_me_stats(oe.e, st.ctypes.data)
         tot += st
     assert (tot > 0).all(), tot
@@ -313,6 +314,56 @@ def test_openh264_md_constants_pinned(oracle):
     oracle.L.h264o_md_constants(out)
     assert list(out) == [c['md_vaa_i4_threshold']['value'], c['md_i4_mode_bits_shift']['value'], c['md_i4_mb_overhead']['value']]
     assert c['md_camera_intra_fine_md']['value'] == 254 and c['md_camera_md_cost_array']['value'] == 84
+
+
+def test_openh264_pskip_constants_pinned(oracle):
+    """The P_Skip judge's constants the oracle applies are the immediates the fixture cites: the skip
+    vector's bounds (func 415), the largest admitted |level|, the luma and chroma single-coefficient cost limits
+    (funcs 415 / 534); and the MB types the judge and the double check compare with (MB_TYPE_SKIP 0x100, 16x16 8)"""
+    c = OH['code_constants']
+    out = (ctypes.c_int32 * 5)()
+    oracle.L.h264o_pskip_constants(out)
+    assert list(out) == [c['pskip_mv_min']['value'], c['pskip_mv_max_low_bits']['value'], c['pskip_max_level']['value'],
+                         c['pskip_luma_single_ctr_max']['value'], c['pskip_chroma_single_ctr_max']['value']]
+    assert c['pskip_mb_type_skip']['value'] == 0x100 and c['pskip_try_nb_type_skip']['value'] == 0x100
+    assert c['pskip_double_check_type']['value'] == 8
+
+
+def _single_ctr_listing(lv):
+    """WelsCalculateSingleCtr4x4 as h264.wasm func 1011 computes it (650906-651280), its locals kept: L1 the last
+    non-zero index, L5 = L1 - 1, L2 the search for the next non-zero index below, L3 the sum of run table entries"""
+    T = OH['tables']['single_ctr_run']['values']
+    L1 = next((k for k in range(15, -1, -1) if lv[k]), None)
+    if L1 is None:
+        return 0
+    L3 = 0
+    while True:
+        L5 = L1 - 1
+        L2 = L5
+        if L1 == 0:
+            return L3 + 3
+        L1 = -1
+        while L2 >= 0:
+            if lv[L2]:
+                L1 = L2
+                break
+            L2 -= 1
+        L3 += T[L5 - L1]
+        if L1 < 0:
+            return L3
+
+
+def test_single_ctr_restatement(oracle):
+    """the oracle's single-coefficient cost (h264o_single_ctr) against the listing's transcription, on sparse level
+    patterns (the judge only scores blocks whose levels are 0 / +-1)"""
+    rng = np.random.default_rng(11)
+    oracle.L.h264o_single_ctr.argtypes = [ctypes.c_void_p]
+    for k in range(2000):
+        lv = (rng.random(16) < rng.random() * 0.5).astype(np.int16) * rng.choice(np.array([-1, 1], np.int16), 16)
+        if k < 16:
+            lv = np.zeros(16, np.int16)
+            lv[k] = 1
+        assert oracle.L.h264o_single_ctr(lv.ctypes.data) == _single_ctr_listing(list(lv)), lv
 
 
 def test_vaa_intra_var_restatement(oracle):

@@ -141,8 +141,23 @@ class Memory:
 
     def read(self, mem, fmt, count):
         n = struct.calcsize('<' + fmt) * count
-        fo = self.file_offset(mem, n)
-        return list(struct.unpack_from(f'<{count}{fmt}', self.b, fo)), fo
+        try:
+            fo = self.file_offset(mem, n)
+            return list(struct.unpack_from(f'<{count}{fmt}', self.b, fo)), fo
+        except ValueError:
+            pass
+        # a table whose tail is zero: the linker ends the data segment at its last non-zero byte and linear memory
+        # starts zeroed, so the bytes past the segment read 0 -- as long as no other segment covers them
+        for k, (fo, sz) in enumerate(self.segs):
+            a = self.addr[k]
+            if a <= mem < a + sz:
+                for k2, (_, sz2) in enumerate(self.segs):
+                    a2 = self.addr[k2]
+                    if k2 != k and a2 < mem + n and a + sz < a2 + sz2:
+                        raise ValueError(f'address {mem} (+{n}) spans two data segments')
+                raw = self.b[fo + (mem - a):fo + sz] + bytes(n - (a + sz - mem))
+                return list(struct.unpack_from(f'<{count}{fmt}', raw, 0)), fo + (mem - a)
+        raise ValueError(f'address {mem} (+{n}) is not inside a data segment')
 
 
 # name: (linear-memory address, struct format, shape, meaning)
@@ -172,7 +187,11 @@ TABLES = {
     'i4_avail_modes': (43120, 'b', (16, 16), 'g_kiIntra4AvailMode[availability index]: the Intra4x4 modes in order '
                        '(0..8 the standard\'s, 9 DC_L, 10 DC_T, 11 DC_128)'),
     'i4_mode_map': (42976, 'b', (16,), 'g_kiMapModeI4x4: the syntax mode (Intra4x4PredMode) of each internal mode'),
-    'level_limits': (63120, 'i', (17, 8), 'g_ksLevelLimits {level_idc, MaxMBPS, MaxFS, MaxDpbMbs, MaxBR, MaxCPB, MinVmv, MaxVmv} '
+    # P_Skip judge (oracle pskip_judge, GPU pskip_test_4w / _3w)
+    'single_ctr_run': (40656, 'i', (16,), 'WelsCalculateSingleCtr4x4 (func 1011) cost per nonzero level by the run of zeros below '
+                       'it in scan order (JVT-O079)'),
+    'chroma_qp': (55152, 'B', (52,), 'g_kuiChromaQpTable: chroma QP of min(51, luma QP + chroma_qp_index_offset) (func 534)'),
+    'level_limits': (63120, 'i', (17, 8),'g_ksLevelLimits {level_idc, MaxMBPS, MaxFS, MaxDpbMbs, MaxBR, MaxCPB, MinVmv, MaxVmv} '
                      '(WelsInitSps, func 280, walks it in this order)'),
 }
 
@@ -235,6 +254,22 @@ CODE_CONSTANTS = {
                             'MB\'s 4x4-mean variance (func 854) is above this'),
     'md_i4_mode_bits_shift': (475108, 'i32.const', 774, 'WelsMdI4x4Fast: a mode other than the predicted one costs lambda << this'),
     'md_i4_mb_overhead': (476981, 'i32.const', 774, 'WelsMdI4x4Fast: the I4x4 MB costs its blocks + lambda * this'),
+    # P_Skip judge: WelsMdInterMb func 746, WelsMdPSkipEnc func 415, PredictSadSkip func 331,
+    # WelsTryPUVskip func 534, WelsMdInterSecondaryModesEnc's double check func 399
+    'pskip_mb_type_skip': (235007, 'i32.const', 415, 'MB_TYPE_SKIP: the co-located MB of a P reference picture must be of '
+                           'this type for its skip SAD to admit the skip'),
+    'pskip_try_nb_type_skip': (470843, 'i32.const', 746, 'WelsMdInterMb: without a skipped neighbour the skip is tried only '
+                               'when the co-located MB of a P reference picture has this type (or MB_TYPE_BACKGROUND)'),
+    'pskip_mv_min': (234693, 'i32.const', 415, 'WelsMdPSkipEnc: no skip when (mv >> 2) + 16 * mb position is below this'),
+    'pskip_mv_max_low_bits': (234709, 'i32.const', 415, 'WelsMdPSkipEnc: ... or above (16 * MBs across | this)'),
+    'pskip_max_level': (235268, 'i32.const', 415, 'WelsMdPSkipEnc: a luma 4x4 block whose largest |level| exceeds this '
+                        'rejects the skip'),
+    'pskip_luma_single_ctr_max': (235324, 'i32.const', 415, 'WelsMdPSkipEnc: the MB\'s summed single-coefficient cost of '
+                                  'luma blocks may be at most this'),
+    'pskip_chroma_single_ctr_max': (281767, 'i32.const', 534, 'WelsTryPUVskip: a chroma plane\'s summed single-coefficient '
+                                    'cost may be at most this'),
+    'pskip_double_check_type': (217889, 'i32.const', 399, 'WelsMdInterDoubleCheckPskip: only an MB of this type '
+                                '(MB_TYPE_16x16) with cbp 0 at the skip vector becomes P_Skip'),
     # stream syntax (oracle h264o_write_sps / h264o_enc_encode)
     'sps_log2_max_frame_num_and_poc_type': (167923, 'i64.const', 280, 'WelsInitSps: one i64 store of '
                                             '{uiLog2MaxFrameNum (low word), uiPocType (high word)}'),
