@@ -66,7 +66,7 @@ static void round_trip(int w, int h, int br, int nf, int skip) {
         int32_t mi[8 * 4];
         if ((size_t)((w + 15) / 16) * ((h + 15) / 16) <= 4) { h264o_enc_mbinfo(e, mi); h264o_dec_mbinfo(d, mi); }
     }
-    int32_t st[5];
+    int32_t st[6];
     h264o_enc_me_stats(e, st);
     (void)h264o_enc_frames_skipped(e);
     (void)h264o_enc_last_qp(e);

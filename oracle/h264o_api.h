@@ -32,8 +32,9 @@ void h264o_enc_set_frame_skip(H264OEnc *e, int enable);
 int h264o_enc_frames_skipped(const H264OEnc *e);
 /* motion-search stage counters since creation: cross searches run, cross searches that moved the
  * vector, start points won by a neighbour candidate (A, B or C) */
-/* {cross searches, cross searches that moved, neighbour start points won, P_Skip judges run, double-check skips} */
-void h264o_enc_me_stats(const H264OEnc *e, int32_t out[5]);
+/* {cross searches, cross searches that moved, neighbour start points won, P_Skip judges run, double-check skips,
+ * intra MBs in P slices} */
+void h264o_enc_me_stats(const H264OEnc *e, int32_t out[6]);
 /* WelsCalculateSingleCtr4x4 (h264.wasm func 1011) over 16 levels in scan order */
 int h264o_single_ctr(const int16_t lv[16]);
 /* {mv min, mv max low bits, max level, luma single-ctr max, chroma single-ctr max} */

@@ -118,7 +118,7 @@ struct H264OEnc {
     /* per MB, the P_Skip judge's memory (func 734): the skip SAD (luma + chroma SAD of the prediction at the skip
      * vector) of a skipped MB, -1 for any other; this frame's and the reference picture's (last coded frame) */
     int32_t *sksad_cur, *sksad_ref;
-    int stat_cross, stat_cross_moved, stat_nb_start, stat_skip_tried, stat_skip_double;  /* ME path counters (tests: coverage of the search stages) */
+    int stat_cross, stat_cross_moved, stat_nb_start, stat_skip_tried, stat_skip_double, stat_intra_p;  /* ME path counters (tests: coverage of the search stages) */
 };
 
 /* ---------------- rate control ---------------- */
@@ -728,20 +728,6 @@ static void chroma_intra(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
     encode_chroma(e, mb, mbx, mby, pred, 1);
 }
 
-/* I16x16 best mode by SATD (ties -> lower mode index) */
-static int i16_best(H264OEnc *e, int mbx, int mby, const IntraNb *nb, int *cost, uint8_t pred[256]) {
-    const uint8_t *src = e->src[0] + mby * 16 * e->cw + mbx * 16;
-    int best = -1, bc = 0;
-    uint8_t p[256];
-    for (int m = 0; m < 4; m++) {
-        if (!pred16x16_avail(nb, m)) continue;
-        pred16x16(nb, m, p);
-        int c = satd16x16(src, e->cw, p, 16);
-        if (best < 0 || c < bc) { best = m; bc = c; memcpy(pred, p, 256); }
-    }
-    *cost = bc;
-    return best;
-}
 static void encode_i16(H264OEnc *e, MBInfo *mb, int mbx, int mby, int mode, const uint8_t pred[256]) {
     const uint8_t *src = e->src[0] + mby * 16 * e->cw + mbx * 16;
     uint8_t *dst = e->rec[0] + mby * 16 * e->cw + mbx * 16;
@@ -1034,6 +1020,16 @@ static int predict_sad_skip(const H264OEnc *e, int mbx, int mby) {
     default: return sA + sB + sC - imin(sA, imin(sB, sC)) - imax(sA, imax(sB, sC));
     }
 }
+/* WelsMdI16x16's cost (func 313: SAD + lambda x mode bits, the first minimum in the pinned order) of the MB against its
+ * reconstructed neighbours -- WelsMdFirstIntraMode's (func 747) first step in P slices */
+static int i16_cost_oh(H264OEnc *e, int mbx, int mby, int lam) {
+    IntraNb nb;
+    uint8_t p16[256];
+    int c16;
+    get_nb16(e->rec[0], e->cw, mbx * 16, mby * 16, 16, mby > 0, mbx > 0, &nb);
+    i16_best_oh(e, mbx, mby, &nb, lam, &c16, p16);
+    return c16;
+}
 static int sad_mb_pred(H264OEnc *e, int mbx, int mby, const uint8_t pl[256], uint8_t pc[2][64]) {
     const int cs = e->cw / 2;
     return sad_blk(e->src[0] + mby * 16 * e->cw + mbx * 16, e->cw, pl, 16, 16, 16) +
@@ -1051,8 +1047,10 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
      * neighbour (left, top, top-left, top-right) was skipped, or, on a P reference picture, the co-located MB was;
      * then, unless the skip vector points too far outside the picture, the skip is taken when the prediction's SAD
      * (luma + chroma) is 0, below the neighbours' predicted skip SAD, or (P reference, co-located MB skipped) below
-     * that MB's skip SAD -- else when its residual passes pskip_residual_ok. (OpenH264 then tries the intra modes
-     * unless the left, top and top-right MBs were all skipped; here a taken skip is final: own.) */
+     * that MB's skip SAD -- else when its residual passes pskip_residual_ok. A taken skip is kept outright when the left,
+     * top and top-right MBs were skipped (bKeepSkip); otherwise WelsMdFirstIntraMode (func 747) codes the MB intra
+     * when its I16x16 cost (pinned SAD rule, §3.3) is below the skip's luma SAD (bMdUsingSad: the wrapper's
+     * complexity 0, func 1143 732160) -- I16x16, or Intra4x4 by the same VAA-gated search as in I slices. */
     const int n = mby * e->mbw + mbx, mbw = e->mbw;
     const int ref_p = !e->last_idr, ref_skip = ref_p && e->sksad_ref[n] >= 0;
     const int try_skip = (mbx > 0 && e->mbs[n - 1].type == MBT_PSKIP) || (mby > 0 && e->mbs[n - mbw].type == MBT_PSKIP) ||
@@ -1070,6 +1068,16 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
                          pskip_residual_ok(e, mbx, mby, mb->qp, pl, pc);
         e->stat_skip_tried++;
         if (take) e->sksad_cur[n] = tsad;
+    }
+    if (e->sksad_cur[n] >= 0) {
+        const int keep = mbx > 0 && mby > 0 && mbx + 1 < mbw && e->mbs[n - 1].type == MBT_PSKIP && e->mbs[n - mbw].type == MBT_PSKIP &&
+                         e->mbs[n - mbw + 1].type == MBT_PSKIP;
+        if (!keep && i16_cost_oh(e, mbx, mby, lam) < sad_blk(e->src[0] + mby * 16 * e->cw + mbx * 16, e->cw, pl, 16, 16, 16)) {
+            e->sksad_cur[n] = -1;
+            e->stat_intra_p++;
+            encode_intra_mb(e, mb, mbx, mby);
+            return;
+        }
     }
     if (e->sksad_cur[n] >= 0) {  /* P_Skip: the reconstruction is the prediction */
         for (int p = 0; p < 2; p++)
@@ -1129,7 +1137,15 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
         if (cbx != bx || cby != by) e->stat_cross_moved++;
         bc = cbc; bx = cbx; by = cby;
     }
-    /* 3. half then quarter refinement by SATD */
+    /* 3. WelsMdFirstIntraMode (func 747, called first by WelsMdInterSecondaryModesEnc, func 399): the MB is coded intra
+     * when its I16x16 cost (pinned SAD rule) is below the integer search's cost (here this project's search: SAD +
+     * lambda x mvd bits) -- I16x16, or Intra4x4 by the VAA-gated search; before the sub-pel refinement, as OpenH264 */
+    if (i16_cost_oh(e, mbx, mby, lam) < bc) {
+        e->stat_intra_p++;
+        encode_intra_mb(e, mb, mbx, mby);
+        return;
+    }
+    /* 4. half then quarter refinement by SATD */
     static const int SUB[8][2] = {{0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
     int mx = 4 * bx, my = 4 * by;
     int sc = subpel_cost(e, mbx, mby, mx, my, mvp, lam);
@@ -1140,19 +1156,6 @@ static void encode_p_mb(H264OEnc *e, MBInfo *mb, int mbx, int mby) {
             int c = subpel_cost(e, mbx, mby, cx, cy, mvp, lam);
             if (c < sc) { sc = c; mx = cx; my = cy; }
         }
-    }
-    /* 4. intra 16x16 alternative */
-    IntraNb nb;
-    get_nb16(e->rec[0], e->cw, mbx * 16, mby * 16, 16, mby > 0, mbx > 0, &nb);
-    uint8_t p16[256];
-    int c16;
-    int m16 = i16_best(e, mbx, mby, &nb, &c16, p16);
-    if (c16 + 6 * lam < sc) {
-        for (int i = 0; i < 4; i++) mb->ref[i] = -1;
-        for (int i = 0; i < 16; i++) mb->mv[i][0] = mb->mv[i][1] = 0;
-        encode_i16(e, mb, mbx, mby, m16, p16);
-        chroma_intra(e, mb, mbx, mby);
-        return;
     }
     /* 5. P16x16 */
     mb->type = MBT_P16x16;
@@ -1293,9 +1296,9 @@ int h264o_enc_gom_state(const H264OEnc *e, int32_t *out, int cap) {
     return G;
 }
 int h264o_enc_frames_skipped(const H264OEnc *e) { return e ? e->skipped : 0; }
-void h264o_enc_me_stats(const H264OEnc *e, int32_t out[5]) {
+void h264o_enc_me_stats(const H264OEnc *e, int32_t out[6]) {
     out[0] = e->stat_cross; out[1] = e->stat_cross_moved; out[2] = e->stat_nb_start;
-    out[3] = e->stat_skip_tried; out[4] = e->stat_skip_double;
+    out[3] = e->stat_skip_tried; out[4] = e->stat_skip_double; out[5] = e->stat_intra_p;
 }
 void h264o_enc_force_idr(H264OEnc *e) { if (e) e->force_idr = 1; }
 int h264o_enc_last_qp(const H264OEnc *e) { return e->last_qp; }

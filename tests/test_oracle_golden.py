@@ -150,16 +150,16 @@ def test_frame_skip_and_row_qp_in_stream(oracle):
 def test_motion_search_stages_exercised(oracle):
     """the fixture workloads reach every integer-search stage the GPU is held bit-exact on: start
     points won by a neighbour's vector, cross searches, and cross searches that move the vector; and both
-    ways an MB becomes P_Skip (the judge run, the double check after P16x16 coding)"""
+    ways an MB becomes P_Skip (the judge run, the double check after P16x16 coding) and intra MBs in P slices"""
     from h264mi.synth import SyntheticStream
-    tot = np.zeros(5, np.int64)
-    for sid, (w, h, br) in enumerate([(352, 288, 2000000), (640, 360, 1000000), (352, 288, 30000000)]):
+    tot = np.zeros(6, np.int64)
+    for sid, (w, h, br, nf) in enumerate([(352, 288, 2000000, 5), (640, 360, 1000000, 5), (352, 288, 30000000, 5), (640, 360, 4000000, 8)]):
         g = SyntheticStream(sid, w, h)
         oe = oracle.encoder(w, h, br)
         oe.set_frame_skip(False)
-        for t in range(5):
+        for t in range(nf):
             oe.encode(np.ascontiguousarray(g.frame(t)))
-        st = np.zeros(5, np.int32)
+        st = np.zeros(6, np.int32)
         oracle.L.h264o_enc_me_stats(oe.e, st.ctypes.data)
         tot += st
     assert (tot > 0).all(), tot
