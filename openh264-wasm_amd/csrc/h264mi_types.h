@@ -8,6 +8,7 @@
 
 #define H264MI_MAX_STREAMS 256
 #define H264MI_MB_SLOT_DWORDS 640      // per-MB CAVLC scratch (20480 bits; worst case < 17.6 kbit)
+#define H264MI_ENC_MAX_MBW 512        // widest encoder picture in MBs (8192 samples, runtime_enc.inc enc_create)
 #define H264MI_GRANULES_PER_MB 16      // row-to-row hand-off record (8-byte {tag,payload} granules)
 #define H264MI_DBK_GRANULES_PER_MB 24  // deblocking hand-off (luma rows 12..15, chroma rows 6..7)
 // Encoder reference planes are stored edge-padded (the picture's border samples replicated, the

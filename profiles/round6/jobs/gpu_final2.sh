@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6, final (after the P_Skip judge and the intra alternative were pinned): the whole GPU suite, smoke(), the driver's bench invocation, and rocprofv3 --kernel-trace --stats of the bench
 cd "$(dirname "$0")/../../.." && mkdir -p gpurun_out/eprof
-d=gpurun_out/r6final2; mkdir -p $d
+d=gpurun_out/r6final3; mkdir -p $d
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $d/gpu_tests.txt 2>&1
 rc=$?; tail -3 $d/gpu_tests.txt; [ $rc -ne 0 ] && { echo "tests rc=$rc"; exit $rc; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $d/smoke.txt 2>&1 || { tail -5 $d/smoke.txt; exit 1; }
@@ -14,5 +14,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $root/$d/prof -o run --out
 cd $root && head -6 $d/prof/run_kernel_stats.csv | cut -c1-160
 timeout -k 10 600 python -u bench.py --gpus 1 > $d/bench_240.json 2> $d/bench_240.err || { tail -5 $d/bench_240.err; exit 1; }
 python3 -c "import json; d=json.load(open('$d/bench_240.json')); print('240 steps', d['value'], d['ms_per_step'], str(d['parity']['vs_oracle'])[:160])"
-for v in f g; do [ -f openh264-wasm_amd/lib/ab/libh264mi_prof_$v.so ] && H264MI_LIB=openh264-wasm_amd/lib/ab/libh264mi_prof_$v.so timeout -k 10 300 python -u tools/enc_prof.py 1920 1080 1000000 128 6 > gpurun_out/eprof/encprof_s128_$v.txt 2>&1; done
+
 exit 0
