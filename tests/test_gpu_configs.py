@@ -317,3 +317,32 @@ def test_intra_decision_geometries_vs_oracle(gpu_lib, oracle, w, h):
                 ref = oes[s].encode(clips[t][s])
                 assert n[s] == len(ref) and enc.nal_bytes(s, n[s]) == ref, (br, t, s)
         enc.close()
+
+
+def test_p_slice_decisions_16_streams_vs_oracle(gpu_lib, oracle):
+    """OpenH264's P-slice decisions (the P_Skip judge, its double check, WelsMdFirstIntraMode with
+    Intra4x4 MBs in P slices) on the lean encoder build with per-XCD ticket queues (16 streams of 1080p: every
+    workgroup's judge accumulators, the intra MBs' early decision and top-right polls under real contention -- a
+    judge word cleared while a late wave still read it diverged 1 stream in 16 here before the accumulators were
+    double-buffered): NAL bytes == oracle for 3 frames, and the frames hold intra MBs in P slices"""
+    import torch
+    import h264mi
+    from h264mi.synth import SyntheticStream
+    w, h, br, S = 1920, 1080, 1000000, 16
+    gs = [SyntheticStream(s, w, h) for s in range(S)]
+    enc = h264mi.BatchEncoder(w, h, br, S)
+    enc.set_frame_skip(False)
+    oes = [oracle.encoder(w, h, br) for _ in range(S)]
+    for oe in oes:
+        oe.set_frame_skip(False)
+    for t in range(3):
+        frames = np.stack([np.ascontiguousarray(g.frame(t)) for g in gs])
+        enc.encode(torch.from_numpy(frames).cuda())
+        n = enc.nal_sizes()
+        for s in range(S):
+            ref = oes[s].encode(frames[s])
+            assert n[s] == len(ref) and enc.nal_bytes(s, n[s]) == ref, f'frame {t} stream {s}'
+    st = np.zeros(6, np.int32)
+    oracle.L.h264o_enc_me_stats(oes[0].e, st.ctypes.data)
+    assert st[3] > 0 and st[5] > 0, st  # judges run, intra MBs in P slices
+    enc.close()
