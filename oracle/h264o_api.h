@@ -37,6 +37,9 @@ int h264o_enc_frames_skipped(const H264OEnc *e);
 void h264o_enc_me_stats(const H264OEnc *e, int32_t out[6]);
 /* WelsCalculateSingleCtr4x4 (h264.wasm func 1011) over 16 levels in scan order */
 int h264o_single_ctr(const int16_t lv[16]);
+/* PredictSadSkip (h264.wasm func 331) over the neighbour cache {top-left, top, top-right, left}: reference index (-2
+ * outside, -1 intra, 0 inter), skipped flag, skip SAD */
+int h264o_predict_sad_skip(const int32_t ref[4], const int32_t sk[4], const int32_t sad[4]);
 /* {mv min, mv max low bits, max level, luma single-ctr max, chroma single-ctr max} */
 void h264o_pskip_constants(int32_t out[5]);
 int h264o_rc_row_delta(int64_t row_bits, int64_t mean);

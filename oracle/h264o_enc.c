@@ -995,30 +995,38 @@ static int pskip_residual_ok(H264OEnc *e, int mbx, int mby, int qp, const uint8_
     }
     return 1;
 }
-/* PredictSadSkip (func 331): the skip SAD the neighbours predict -- A left, B top, C top-right (top-left when the
- * top-right MB is outside the picture); a neighbour counts with its skip SAD if it was skipped, else 0. One skipped
- * neighbour: its SAD; otherwise the median of the three. Without a top or top-left MB: the left MB's. */
-static int predict_sad_skip(const H264OEnc *e, int mbx, int mby) {
-    const int mbw = e->mbw, n = mby * mbw + mbx;
-    const int avA = mbx > 0, avB = mby > 0, avC = mby > 0 && mbx + 1 < mbw, avD = mbx > 0 && mby > 0;
-#define SK(av, i) ((av) && e->mbs[i].type == MBT_PSKIP)
-    const int skA = SK(avA, n - 1), skB = SK(avB, n - mbw);
-    int skC = SK(avC, n - mbw + 1);
-    const int sA = skA ? e->sksad_cur[n - 1] : 0, sB = skB ? e->sksad_cur[n - mbw] : 0;
-    int sC = skC ? e->sksad_cur[n - mbw + 1] : 0, avCC = avC;
-    if (!avC) {
-        skC = SK(avD, n - mbw - 1);
-        sC = skC ? e->sksad_cur[n - mbw - 1] : 0;
-        avCC = avD;
-        if (!avB && !avCC && avA) return sA;
+/* PredictSadSkip (func 331) over OpenH264's neighbour cache: index 0 top-left, 1 top, 2 top-right, 3 left; ref the
+ * cached reference index (-2 outside the picture, -1 intra, 0 inter), sk 1 if the MB was skipped, sad its skip SAD. C is
+ * the top-right MB, the top-left one when the top-right is outside the picture; a neighbour counts with its skip SAD if
+ * it was skipped (and inter), else 0. One such neighbour: its SAD; otherwise the median of the three. Without a top or
+ * top-left MB: the left MB's. */
+int h264o_predict_sad_skip(const int32_t ref[4], const int32_t sk[4], const int32_t sad[4]) {
+    int sA = sk[3] ? sad[3] : 0, sB = sk[1] ? sad[1] : 0, sC = sk[2] ? sad[2] : 0;
+    int refC = ref[2], skC = sk[2];
+    if (refC == -2) {
+        refC = ref[0]; skC = sk[0]; sC = sk[0] ? sad[0] : 0;
+        if (ref[1] == -2 && refC == -2 && ref[3] != -2) return sA;
     }
-#undef SK
-    switch (skA | (skB << 1) | (skC << 2)) {
+    const int f = (ref[3] == 0 ? sk[3] : 0) | ((ref[1] == 0 ? sk[1] : 0) << 1) | ((refC == 0 ? (skC ? 4 : 0) : 0));
+    switch (f) {
     case 1: return sA;
     case 2: return sB;
     case 4: return sC;
     default: return sA + sB + sC - imin(sA, imin(sB, sC)) - imax(sA, imax(sB, sC));
     }
+}
+static int predict_sad_skip(const H264OEnc *e, int mbx, int mby) {
+    const int mbw = e->mbw, n = mby * mbw + mbx;
+    const int av[4] = {mbx > 0 && mby > 0, mby > 0, mby > 0 && mbx + 1 < mbw, mbx > 0};
+    const int nb[4] = {n - mbw - 1, n - mbw, n - mbw + 1, n - 1};
+    int32_t ref[4], sk[4], sad[4];
+    for (int i = 0; i < 4; i++) {
+        const MBInfo *m = av[i] ? &e->mbs[nb[i]] : NULL;
+        ref[i] = !m ? -2 : (mb_is_intra(m->type) ? -1 : 0);
+        sk[i] = m && m->type == MBT_PSKIP;
+        sad[i] = sk[i] ? e->sksad_cur[nb[i]] : 0;
+    }
+    return h264o_predict_sad_skip(ref, sk, sad);
 }
 /* WelsMdI16x16's cost (func 313: SAD + lambda x mode bits, the first minimum in the pinned order) of the MB against its
  * reconstructed neighbours -- WelsMdFirstIntraMode's (func 747) first step in P slices */

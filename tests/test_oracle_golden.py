@@ -366,6 +366,59 @@ def test_single_ctr_restatement(oracle):
         assert oracle.L.h264o_single_ctr(lv.ctypes.data) == _single_ctr_listing(list(lv)), lv
 
 
+def _predict_sad_skip_listing(ref, sk, sad):
+    """PredictSadSkip as h264.wasm func 331 computes it (180093-180424), its locals kept: L0 the reference index cache
+    (bytes 0 top-left, 1 top, 5 top-right, 6 left), L1 the skipped flags and L2 the skip SADs (0 top-left, 1 top, 2
+    top-right, 3 left); unavailable -2 (u8 254), intra -1"""
+    u8 = lambda v: v & 255
+    L12 = sk[1]
+    L6 = sad[1] if L12 == 1 else 0
+    L9 = sk[2]
+    L4 = sad[2] if L9 == 1 else 0
+    L7 = u8(ref[2])
+    L13 = sk[3]
+    L5 = sad[3] if L13 == 1 else 0
+    L10, L11 = ref[3], ref[1]
+    if L7 == 254:
+        L9, L4 = 0, 0
+        if sk[0] == 1:
+            L9, L4 = 1, sad[0]
+        L7 = u8(ref[0])
+        if L11 == -2 and L7 == 254 and L10 != -2:
+            return L5
+    idx = (((0 if L10 else L13) | (0 if L11 else (L12 << 1)) | (0 if L7 else (4 if L9 else 0))) - 1) & 0xffffffff
+    if idx == 0:
+        return L5
+    if idx == 1:
+        return L6
+    if idx == 3:
+        return L4
+    lo = min(L5, L6)
+    hi2 = max(L5, L6)
+    mn = L4 if lo > L4 else lo
+    mx = hi2 if lo > L4 else max(hi2, L4)
+    return L5 + L6 + L4 - (mn + mx)
+
+
+def test_predict_sad_skip_restatement(oracle):
+    """the oracle's PredictSadSkip (h264o_predict_sad_skip, used by its P_Skip judge) against the listing's
+    transcription, over every availability / intra / skipped combination of the four neighbours with random SADs"""
+    import itertools
+    rng = np.random.default_rng(5)
+    f = oracle.L.h264o_predict_sad_skip
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    n = 0
+    for states in itertools.product(range(4), repeat=4):  # 0 outside, 1 intra, 2 inter, 3 skipped
+        ref = np.array([-2 if st == 0 else (-1 if st == 1 else 0) for st in states], np.int32)
+        sk = np.array([1 if st == 3 else 0 for st in states], np.int32)
+        for _ in range(3):
+            sad = rng.integers(0, 5000, 4).astype(np.int32)
+            want = _predict_sad_skip_listing([int(v) for v in ref], [int(v) for v in sk], [int(v) for v in sad])
+            assert f(ref.ctypes.data, sk.ctypes.data, sad.ctypes.data) == want, (states, sad)
+            n += 1
+    assert n == 768
+
+
 def test_vaa_intra_var_restatement(oracle):
     """AnalysisVaaInfoIntra (h264.wasm func 854) restated in numpy: the sixteen 4x4 means (sum >> 4), then
     sum of squares - (sum^2 >> 4), on random and flat MBs"""
