@@ -1,7 +1,7 @@
 #!/bin/bash
 # same-box A/B of library builds at the driver's invocation (no CPU leg / PMC), interleaved rounds
 # usage: tools/ab_bench_libs.sh <tag> <rounds> "<extra bench args>" lib...
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 tag=$1; n=$2; extra=$3; shift 3
 out=gpurun_out/abb_${tag}.txt; : > $out
 for r in $(seq 1 $n); do

@@ -2,7 +2,7 @@
 # same-box A/B of two library builds: the encoder timeline at 32 streams (frame spans, row 0 / row 67 lives)
 # and the driver's bench line without the CPU leg or PMC passes, alternating A B A B ...
 # usage: tools/ab_enc.sh <tag> <libA> <libB> [rounds=2]
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 tag=$1; A=$2; B=$3; n=${4:-2}
 out=gpurun_out/ab_${tag}.txt; : > $out
 for r in $(seq 1 $n); do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # encoder rows' wave priority (H264MI_ENC_PRIO) in the full pipeline (decoder beside), interleaved, no CPU leg / PMC
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_prio_bench.txt; : > $out
 for r in 1 2; do
   for p in ${PRIOS:-0 2 3 4}; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # the recon-gate test, then a same-box A/B of bench --recon-gate 0 / 1 at the driver's invocation (no CPU leg / PMC)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py -q -k "recon_gate or 1080p-s4 or pipelined" --timeout 120 --timeout-method thread > gpurun_out/r5_rg_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/r5_rg_tests.log; [ $rc -ne 0 ] && exit $rc
 out=gpurun_out/r5_recon_gate.txt; : > $out

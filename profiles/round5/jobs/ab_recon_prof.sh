@@ -1,7 +1,7 @@
 #!/bin/bash
 # reconstruction section profiles (tools/recon_prof.py, 32 x 1080p, 8 frames) of library builds, same box
 # usage: tools/ab_recon_prof.sh <tag> lib...
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 tag=$1; shift
 out=gpurun_out/rprof_${tag}.txt; : > $out
 for lib in "$@"; do

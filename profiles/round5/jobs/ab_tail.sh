@@ -1,6 +1,6 @@
 #!/bin/bash
 # same-box A/B of the streamed tail (bench --tail-streamed 0 / 1) at the driver's invocation, interleaved
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_tail.txt; : > $out
 for r in 1 2; do
   for ts in 0 1; do

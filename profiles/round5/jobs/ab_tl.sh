@@ -1,7 +1,7 @@
 #!/bin/bash
 # same-box comparison of several library builds by the encoder timeline alone (32 x 1080p, frames 3..5: span and
 # row 0's life), interleaved over rounds.   usage: tools/ab_tl.sh <tag> <rounds> lib...
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 tag=$1; n=$2; shift 2
 out=gpurun_out/abtl_${tag}.txt; : > $out
 for r in $(seq 1 $n); do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # like ab_tl.sh, printing the frame span and the lives of rows 0 / 63 / 67 (encoder timeline, 32 streams, frames 3..5)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 tag=$1; n=$2; shift 2
 out=gpurun_out/abtr_${tag}.txt; : > $out
 for r in $(seq 1 $n); do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # same-box A/B of the per-XCD ticket queues (H264MI_ENC_XQ) with the in-run traffic passes, interleaved
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_xq.txt; : > $out
 for r in 1 2; do
   for xq in 0 1; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # per-XCD ticket queues at higher stream counts (no CPU leg, no PMC), interleaved
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_xq_cap.txt; : > $out
 for S in 64 128; do
   for r in 1 2; do

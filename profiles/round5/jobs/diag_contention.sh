@@ -1,7 +1,7 @@
 #!/bin/bash
 # what slows the encoder inside the pipeline: the bench as is, encode only on the masked wavefront CUs, encode
 # only on every CU (no CPU leg / PMC)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_contention.txt; : > $out
 for r in 1 2; do
   for cfg in "full:" "enc-masked:--no-decode" "enc-all:--no-decode --parse-cus 0"; do

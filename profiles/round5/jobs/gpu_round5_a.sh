@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 GPU call: the -m gpu suite, then (if the suite ended normally: pass or test failures) the
 # encoder's section profile at 32 streams
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 timeout -k 10 840 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r5_gputest.log 2>&1
 rc=$?
 tail -3 gpurun_out/r5_gputest.log

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 GPU call: encoder timeline at 8 and 16 streams (contention), bench at 32 / 48 / 64 streams per GPU
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_capacity.txt; : > $out
 for S in 8 16; do
   echo "== timeline S=$S" >> $out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 GPU call: encoder parity tests, section profiles (all rows, rows 0 and 67), the driver's bench line
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 tag=${1:-f}
 timeout -k 10 400 python -u -m pytest tests/test_gpu_encoder.py tests/test_gpu_configs.py tests/test_gpu_batch.py -q --timeout 120 --timeout-method thread > gpurun_out/r5${tag}_enc_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/r5${tag}_enc_tests.log

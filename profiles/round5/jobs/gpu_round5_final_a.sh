@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 final evidence, part A: the whole GPU test suite, smoke(), the driver's bench invocation (CPU leg + PMC passes)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 d=gpurun_out/final5; mkdir -p $d
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $d/gpu_tests.txt 2>&1
 rc=$?; tail -3 $d/gpu_tests.txt; [ $rc -ne 0 ] && { echo "tests rc=$rc"; exit $rc; }

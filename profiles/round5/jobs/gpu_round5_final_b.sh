@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 final evidence, part B: rocprofv3 kernel trace + stats of the bench, SQ wave states, encoder section
 # profiles (all rows, rows 0 / 67, detail build), the encoder timeline at 32 streams
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 d=gpurun_out/final5; mkdir -p $d
 ./tools/gpu_trace.sh final5/trace > /dev/null || exit $?
 f=$(find $d/trace -name '*kernel_stats.csv' | head -1); cp $f $d/kernel_stats.csv

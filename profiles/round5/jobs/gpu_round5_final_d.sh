@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 final evidence, part D: C-ABI latency over 24 frames at 8 Mbps (the frame-22 scene change
 # included, round 4's 87 ms maximum), the 8 Mbps bench line, and the default 240-step bench (drain amortised)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 d=gpurun_out/final5; mkdir -p $d
 timeout -k 10 240 python -u tools/capi_latency.py 1920 1080 8000000 24 > $d/capi_8m_24.json 2> $d/capi_8m_24.err || { tail -5 $d/capi_8m_24.err; exit 1; }
 tail -c 330 $d/capi_8m_24.json

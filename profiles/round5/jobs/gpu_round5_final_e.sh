@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 final evidence, part E (after the reconstruction changes): rocprofv3 kernel trace + stats of the
 # bench and the SQ wave states (part B without the encoder-only profiles, which the decoder does not change)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 d=gpurun_out/final5; mkdir -p $d
 ./tools/gpu_trace.sh final5/trace > /dev/null || exit $?
 f=$(find $d/trace -name '*kernel_stats.csv' | head -1); cp $f $d/kernel_stats.csv

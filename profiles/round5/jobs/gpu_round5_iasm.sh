@@ -1,7 +1,7 @@
 #!/bin/bash
 # I slices in the asm macroblock run: GPU tests, then the IDR / scene-change slice parse times of the
 # previous library ($1) and this one, then a same-box bench A/B
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 base=${1:-openh264-wasm_amd/lib/libh264mi_base.so}
 new=openh264-wasm_amd/lib/libh264mi.so
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5i_tests.txt 2>&1 || { tail -30 gpurun_out/r5i_tests.txt; exit 1; }

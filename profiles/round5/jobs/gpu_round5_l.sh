@@ -1,6 +1,6 @@
 #!/bin/bash
 # a reconstruction variant library ($1): section profile vs the previous build, GPU tests on it, bench A/B
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 v=$1; tag=${TAG:-var}
 ./tools/ab_recon_prof.sh $tag openh264-wasm_amd/lib/libh264mi_pre.so $v > /dev/null || exit 1
 grep "frame 4\|dec_recon\|==" gpurun_out/rprof_$tag.txt

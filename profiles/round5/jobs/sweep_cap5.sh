@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 capacity sweep: streams per GPU x reserved parse CUs, the driver's 20 / 5 steps (no CPU leg, no PMC)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_cap_sweep.txt; : > $out
 for cfg in "64 48" "64 64" "96 48" "96 64" "128 64" "128 96"; do
   set -- $cfg

@@ -1,6 +1,6 @@
 #!/bin/bash
 # decode group size sweep (frames per decode call) at the driver's invocation (no CPU leg / PMC), interleaved
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_group.txt; : > $out
 for r in 1 2; do
   for g in ${GS:-2 4 8}; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # encoder / decoder group sweep at the driver's invocation (no CPU leg, no PMC), interleaved rounds
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_groups.txt; : > $out
 for r in 1 2; do
   for cfg in ${CFGS:-1:1 2:1 4:1}; do

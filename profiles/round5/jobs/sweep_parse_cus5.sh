@@ -1,6 +1,6 @@
 #!/bin/bash
 # parse-CU reservation sweep at the driver's invocation (no CPU leg / PMC), interleaved rounds
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_parse_cus.txt; : > $out
 for r in ${RS:-1 2}; do
   for pc in ${PCS:-24 32 40}; do

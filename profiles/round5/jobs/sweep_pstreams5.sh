@@ -1,6 +1,6 @@
 #!/bin/bash
 # parse-stream count sweep (HIP streams the decoder rotates entropy decoding over) at the driver's invocation (no CPU leg / PMC), interleaved
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_pstreams.txt; : > $out
 for r in 1 2; do
   for g in ${GS:-2 3 4}; do

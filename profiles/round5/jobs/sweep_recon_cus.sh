@@ -1,6 +1,6 @@
 #!/bin/bash
 # reconstruction on its own CU lane (bench --recon-cus) against sharing the encoder's CUs (no CPU leg / PMC)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_recon_cus.txt; : > $out
 for r in 1 2; do
   for rc in ${RCS:-0 32 64 96}; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # bench --recon-gate fraction sweep (no CPU leg / PMC), interleaved rounds
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/r5_recon_gate_frac.txt; : > $out
 for r in 1 2; do
   for f in ${FRACS:-off 0.5 0.75 1.0}; do
