@@ -377,14 +377,21 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
 
 // one granule per lane, already loaded into x (e.g. one step ahead); lanes with need poll it until its
 // tag is epoch. Returns false on abort/timeout.
+// Every exit is preceded by an explicit vmcnt(0) wait, free at run time (the test that ends the loop has just waited
+// for the last reload, the youngest memory operation). Without it the compiler's wait analysis saw a path that left
+// the loop with a reload still in flight (the exits share a block) and charged its destination registers as pending
+// to the rest of the MB loop: a vmcnt(0) on the P path's first write of them, next MB, which then also waited for that
+// MB's window prefetch and the previous MB's output stores (~1 us a MB; profiles/round6/eprof/README).
+#define H264MI_WAIT_VM0() __builtin_amdgcn_s_waitcnt(0x0F70)  // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
 template <class P> DEV bool gran_poll(P g, bool need, uint32_t epoch, uint64_t &x, int32_t *abort_word) {
     WaitClock wc;
     for (unsigned spins = 0;; spins++) {
-        if (__all(!need || (uint32_t)(x >> 32) == epoch)) return true;
+        if (__all(!need || (uint32_t)(x >> 32) == epoch)) { H264MI_WAIT_VM0(); return true; }
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (ab || wc.expired()) {
                 if ((threadIdx.x & 63) == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                H264MI_WAIT_VM0();
                 return false;
             }
         }
