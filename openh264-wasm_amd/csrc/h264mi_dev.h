@@ -383,10 +383,13 @@ template <class P> DEV bool gran_wait(P g, int n, uint32_t epoch, uint32_t *v, i
 // to the rest of the MB loop: a vmcnt(0) on the P path's first write of them, next MB, which then also waited for that
 // MB's window prefetch and the previous MB's output stores (~1 us a MB; profiles/round6/eprof/README).
 #define H264MI_WAIT_VM0() __builtin_amdgcn_s_waitcnt(0x0F70)  // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
+// The first test is outside the loop: a granule set loaded well ahead (and already waited for) is used with no wait
+// at all -- a test at the loop's head waited for whatever the loop's reload left pending, i.e. vmcnt(0) on entry too.
 template <class P> DEV bool gran_poll(P g, bool need, uint32_t epoch, uint64_t &x, int32_t *abort_word) {
+    if (__all(!need || (uint32_t)(x >> 32) == epoch)) return true;
     WaitClock wc;
     for (unsigned spins = 0;; spins++) {
-        if (__all(!need || (uint32_t)(x >> 32) == epoch)) { H264MI_WAIT_VM0(); return true; }
+        if (spins > 0 && __all(!need || (uint32_t)(x >> 32) == epoch)) { H264MI_WAIT_VM0(); return true; }
         if ((spins & 255) == 255) {
             int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (ab || wc.expired()) {
